@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Headline benchmark: NT-Xent fwd+bwd samples/s, B=4096 per view per GPU, d=2048, bf16.
+
+BASELINE.json metric: "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X".
+One rank per GPU (torchrun); for N>1 negatives are gathered over RCCL/xGMI, so each GPU's
+similarity work grows with N (global batch = N * 4096 pairs) while its own batch is fixed
+(weak scaling). A "sample" is one positive pair. Inputs are synthetic random-normal
+embeddings (no dataset); the timed region is the complete loss forward + backward
+(gradient w.r.t. the embeddings) of every step.
+
+  python bench.py [--gpus N --steps K --warmup W --batch 4096 --dim 2048 --dtype bf16]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publishes no numbers
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="pairs (per view) per GPU")
+    ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    ap.add_argument("--compute", default="auto", choices=["auto", "fp16", "bf16", "fp32"])
+    ap.add_argument("--temperature", type=float, default=0.07)
+    ap.add_argument("--recompute", action="store_true", help="recompute logits in backward")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world != 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import ntxent_amd
+    from ntxent_amd.parallel import dist_ntxent_loss
+
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    R = 2 * a.batch
+    h = torch.randn(R, a.dim, device=dev, dtype=dt, generator=g).requires_grad_(True)
+
+    def step():
+        if world > 1:
+            loss = dist_ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute,
+                                    overlap=not a.no_overlap)
+        else:
+            loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute)
+        (gh,) = torch.autograd.grad(loss, h)
+        return loss, gh
+
+    for _ in range(a.warmup):
+        loss, gh = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss, gh = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt_s = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt_s], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_s = float(t.item())
+    ms = dt_s / a.steps * 1e3
+    samples = world * a.batch
+    value = samples / (ms / 1e3)
+    lossv = float(loss.item())
+    if not (lossv == lossv) or not torch.isfinite(gh).all():
+        raise SystemExit("non-finite loss or gradient")
+    from ntxent_amd.ops.reference import flops_fwd_bwd
+
+    tflops = flops_fwd_bwd(R, world * R, a.dim) / (ms / 1e3) / 1e12
+    if rank == 0:
+        out = {
+            "metric": "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
+            "dtype": a.dtype,
+            "data": "synthetic random-normal embeddings",
+            "config": {
+                "model": "NT-Xent loss (SimCLR), fused MFMA fwd+bwd",
+                "global_batch": world * a.batch,
+                "seq_len": None,
+                "batch_per_gpu": a.batch,
+                "dim": a.dim,
+                "temperature": a.temperature,
+                "compute": a.compute,
+                "keep_logits": not a.recompute,
+                "parallelism": f"dp{world}",
+            },
+            "loss": lossv,
+            "tflops_per_gpu_useful": round(tflops, 1),
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            Path(a.json_out).write_text(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,162 @@
+// ntxent-mi355x — public C++ API (raw device pointers, no libtorch dependency).
+//
+// MI355X-native (gfx950 / CDNA4) NT-Xent (SimCLR) loss. This header replaces the
+// reference's `include/ntxent_kernel.cuh` (decls at :31-52, constants :10-13,
+// CUDA_CHECK :16-22, utils :79-110, cuBLAS singleton :112-135) with an API that is
+// correct for the *intended* math and shaped for MI355X:
+//
+//   * one 256x256 MFMA tile per workgroup (8 wave64s), K staged 128 B/row per step
+//     through LDS by global_load_lds (no BLAS in the hot path);
+//   * the 2N x 2N logits are never materialised in fp32: the forward GEMM reduces each
+//     tile to per-row (max, sum-exp2) partials in its epilogue and (optionally) keeps
+//     the cosine tile in the compute dtype for the backward;
+//   * S is symmetric, so within a rank's own column block only the upper-triangular
+//     tiles are computed; each produces row AND column partials;
+//   * the backward is rank-local: C = P + P^T - 2*I_pos is formed from the stored
+//     cosines + all-gathered LSE (no atomics, deterministic), then dZ = C * Z runs on
+//     MFMA; a fused row kernel applies grad_out/(2N*tau) and the L2-normalisation
+//     backward.
+//
+// Layout conventions (see Geometry):
+//   * R local rows = [view1 (n rows); view2 (n rows)], positive p(i) = (i + n) mod R.
+//   * Global column index = rank * Rpad + local row (padded rank blocks).
+//   * Zq   [Rpad][dim_k]     normalised rows in the compute dtype (zero padded).
+//   * ZqT  [dim_n][Rpad]     its transpose (B operand of the dZ GEMM).
+//   * SC   [row_tiles][col_tiles][256*256]  tile-blocked cosines / coefficients.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace ntxent {
+
+// ---- gfx950 constants (reference `WARP_SIZE=32` etc. at include/ntxent_kernel.cuh:10-13
+//      are CUDA-isms; CDNA4 is wave64 with 160 KiB LDS per CU) -------------------------
+constexpr int kWaveSize = 64;
+constexpr int kTile = 256;          // square output tile of every similarity GEMM
+constexpr int kTileElems = kTile * kTile;
+constexpr int kKStepBytes = 128;    // bytes of K staged per row per pipeline step
+constexpr int kGemmThreads = 512;   // 8 waves: 2 (M) x 4 (N), 128x64 per wave
+constexpr int kLdsPerCU = 160 * 1024;
+constexpr int kNumXcd = 8;
+
+enum class DType : int { F32 = 0, F16 = 1, BF16 = 2 };
+
+inline size_t dtype_size(DType t) { return t == DType::F32 ? 4 : 2; }
+inline const char* dtype_name(DType t) {
+  return t == DType::F32 ? "fp32" : (t == DType::F16 ? "fp16" : "bf16");
+}
+
+// Status-typed error check (the reference mis-types a cuBLAS status into AT_CUDA_CHECK at
+// src/ntxent_kernel.cu:166; here every HIP call goes through a hipError_t check).
+#define NTXENT_HIP_CHECK(expr)                                                        \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess) {                                                           \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +   \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__) +   \
+                               " in " #expr);                                         \
+    }                                                                                 \
+  } while (0)
+
+#define NTXENT_CHECK(cond, msg)                                                       \
+  do {                                                                                \
+    if (!(cond)) throw std::invalid_argument(std::string("ntxent: ") + (msg));        \
+  } while (0)
+
+// Problem geometry shared by every kernel of one NT-Xent evaluation.
+struct Geometry {
+  int rows = 0;        // R: local rows (2 * per-view batch on this rank)
+  int rows_pad = 0;    // Rpad = roundup(R, 256)
+  int dim = 0;         // d
+  int dim_k = 0;       // roundup(d, 64): row stride of Zq (K of the forward GEMM)
+  int dim_n = 0;       // roundup(d, 256): rows of ZqT (N of the dZ GEMM)
+  int world = 1;       // W ranks sharing negatives
+  int rank = 0;
+  int row_tiles = 0;   // Rpad / 256
+  int col_tiles = 0;   // W * Rpad / 256
+  float temperature = 0.07f;
+  float inv_temp = 1.0f / 0.07f;
+  long long global_rows = 0;  // W * R  (the 2N of the loss normalisation)
+};
+
+Geometry make_geometry(int rows, int dim, int world, int rank, float temperature);
+
+// Tile kinds of the forward / coefficient pass.
+enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2 };
+
+// Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only.
+std::vector<int4> build_fwd_tiles(const Geometry& g);
+// dZ tiles (ti, tn, ks, 0) for a split-K factor.
+std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit);
+// Split-K factor that fills `num_cus` compute units with dZ tiles.
+int choose_dz_ksplit(const Geometry& g, int num_cus);
+
+// ---- device-side launchers (all asynchronous on `stream`, no host syncs, no mallocs:
+//      safe under hipGraph capture) -----------------------------------------------------
+
+// Row L2-normalisation prologue: inv[i] = 1/max(||h_i||, 1e-12); zq = h*inv (compute
+// dtype, zero padded to dim_k); ypos[i] = <zq_i, zq_p(i)> * inv_temp * log2(e).
+// Pad rows [R, Rpad) of zq are zeroed.
+void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
+                 const Geometry& g, hipStream_t stream);
+
+// zqt[e][j] = zq[j][e] (zero for e >= dim_k). zqt is [dim_n][Rpad].
+void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g,
+                      hipStream_t stream);
+
+// Forward similarity GEMM: tiles of S = zq_local * zq_all^T with the per-row (max, sum)
+// partials epilogue written to part[col_tile][Rpad] (log2 domain). If `sc` is non-null the
+// cosine tile is kept (compute dtype, fragment order) for the backward.
+void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
+                      const int4* tiles, int ntiles, float2* part, void* sc,
+                      const Geometry& g, hipStream_t stream);
+
+// Merge partials -> lse2 (log2 units) into lse2_all[rank*Rpad + i]; loss_sum[0] receives
+// sum_i (lse_i - S_i,p(i)) / (W*R) over this rank's rows (all-reduce SUM across ranks
+// gives the loss). `block_loss` is scratch of Rpad/256 floats.
+void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* block_loss,
+                float* loss_sum, const Geometry& g, hipStream_t stream);
+
+// In-place: stored cosine tiles -> coefficient tiles C = P + P^T - 2 I_pos (row-major per
+// 256x256 tile; mirrors upper-triangular tiles of the own-rank block).
+void launch_coef(DType comp, void* sc, const float* lse2_all, const int4* tiles, int ntiles,
+                 const Geometry& g, hipStream_t stream);
+
+// Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `sc`.
+void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* sc,
+                      const float* lse2_all, const int4* tiles, int ntiles, const Geometry& g,
+                      hipStream_t stream);
+
+// dZ slabs: slabs[ks][Rpad][dim_n] = C[:, K-range ks] * Z[K-range ks, :] (fp32).
+// zqt_all is [W][dim_n][Rpad] (all-gathered ZqT blocks).
+void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles,
+               int ntiles, int ksplit, float* slabs, const Geometry& g, hipStream_t stream);
+
+// dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
+void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,
+                     const float* inv, const float* grad_out, void* dh, const Geometry& g,
+                     hipStream_t stream);
+
+// ---- device utilities (reference utils::get_optimal_block_size / check_tensor_core_support
+//      at include/ntxent_kernel.cuh:80-110) ------------------------------------------------
+struct DeviceInfo {
+  int device = 0;
+  int num_cus = 0;
+  int lds_per_block = 0;
+  int warp_size = 0;
+  std::string arch;  // gcnArchName, e.g. "gfx950:sramecc+:xnack-"
+  bool is_gfx950 = false;
+};
+const DeviceInfo& device_info(int device);  // cached per device
+// True when the device has matrix cores usable by these kernels (gfx950 MFMA).
+bool check_matrix_core_support(int device);
+// Launch config a kernel family would use for `rows` rows (parity with the reference's
+// get_optimal_block_size, which is undefined there: include/ntxent_kernel.cuh:92).
+int get_optimal_block_size(int rows);
+
+}  // namespace ntxent

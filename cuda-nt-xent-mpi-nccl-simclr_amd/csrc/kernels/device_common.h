@@ -1,0 +1,134 @@
+// Device helpers for the gfx950 NT-Xent kernels: vector types, MFMA wrappers, wave64
+// reductions (DPP row ops, no 32-lane masks — cf. the reference's WARP_SIZE=32 and
+// 0xffffffff shuffles at src/ntxent_kernel.cu:17-18,31), dtype conversions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ntxent {
+namespace dev {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf168 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kNumXcdDev = 8;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kNegInf = -__builtin_huge_valf();
+
+// ---- dtype conversion --------------------------------------------------------------
+template <typename T> __device__ __forceinline__ float to_f32(T x);
+template <> __device__ __forceinline__ float to_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ float to_f32<_Float16>(_Float16 x) { return (float)x; }
+template <> __device__ __forceinline__ float to_f32<__bf16>(__bf16 x) { return (float)x; }
+
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ _Float16 from_f32<_Float16>(float x) { return (_Float16)x; }
+template <> __device__ __forceinline__ __bf16 from_f32<__bf16>(float x) { return (__bf16)x; }
+
+// ---- MFMA: one 16-byte K-chunk per lane per operand ----------------------------------
+// 16x16x32 f16/bf16: lane l holds A[row l&15][k 8(l>>4)..+7], B[k ...][col l&15];
+// C/D: col = l&15, row = 4(l>>4) + reg.
+// f32: the same 16-byte chunk (4 consecutive k) drives four 16x16x4 MFMAs; A and B use the
+// identical k permutation so the contraction is exact.
+template <typename T> struct Mfma;
+template <> struct Mfma<_Float16> {
+  typedef half8 frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<__bf16> {
+  typedef bf168 frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<float> {
+  typedef f32x4 frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+    return c;
+  }
+};
+
+// ---- wave64 cross-lane reductions ----------------------------------------------------
+// DPP row_ror within a 16-lane row: 0x120 + n.
+template <int CTRL> __device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+// Reduce across the 16 lanes of a DPP row (lanes sharing l>>4): every lane gets the result.
+__device__ __forceinline__ float row16_max(float x) {
+  x = fmaxf(x, dpp_f<0x128>(x));
+  x = fmaxf(x, dpp_f<0x124>(x));
+  x = fmaxf(x, dpp_f<0x122>(x));
+  x = fmaxf(x, dpp_f<0x121>(x));
+  return x;
+}
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<0x128>(x);
+  x += dpp_f<0x124>(x);
+  x += dpp_f<0x122>(x);
+  x += dpp_f<0x121>(x);
+  return x;
+}
+// Reduce across lanes l, l^16, l^32, l^48 (the 4 DPP rows).
+__device__ __forceinline__ float xrow_max(float x) {
+  x = fmaxf(x, __shfl_xor(x, 16, 64));
+  x = fmaxf(x, __shfl_xor(x, 32, 64));
+  return x;
+}
+__device__ __forceinline__ float xrow_sum(float x) {
+  x += __shfl_xor(x, 16, 64);
+  x += __shfl_xor(x, 32, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+  x = row16_sum(x);
+  return xrow_sum(x);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fast_log2(float x) { return __builtin_amdgcn_logf(x); }
+
+// Merge two (max, sum) online-softmax states in the log2 domain.
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == kNegInf) return;  // both empty
+  s = s * fast_exp2(m - mn) + s2 * fast_exp2(m2 - mn);
+  m = mn;
+}
+
+// Block-wide sum for up to 1024 threads; `red` must hold >= 16 floats. All threads get it.
+__device__ __forceinline__ float block_sum(float x, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  x = wave_sum(x);
+  __syncthreads();
+  if (lane == 0) red[w] = x;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];  // fixed order: deterministic
+  return t;
+}
+
+// XCD-aware, bijective blockIdx remap: blocks that the dispatcher round-robins onto one
+// XCD (b % 8) get a contiguous run of the tile list so neighbouring tiles share L2 panels
+// (cdna_hip_programming.md §5.5 T1, bijective form).
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  if (nwg < 2 * kNumXcdDev) return b;
+  const int q = nwg / kNumXcdDev, r = nwg % kNumXcdDev;
+  const int xcd = b % kNumXcdDev, idx = b / kNumXcdDev;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace dev
+}  // namespace ntxent

@@ -1,0 +1,389 @@
+// PyTorch (ROCm) op layer + Python binding of the MI355X NT-Xent kernels.
+//
+// Replaces the reference's host launchers (src/ntxent_kernel.cu:138-239) and its pybind11
+// bindings (src/binding_new.cpp:4-21): same Python names and kwargs (`forward`, `backward`,
+// `check_tensor_core_support`), plus
+//   * TORCH_LIBRARY registration under `ntxent_cuda` (what python/test.py:137 expects) and
+//     under `ntxent`;
+//   * stage-level ops (prep / fwd_stats / lse / coef / dz / norm_bwd) over a cached `Plan`
+//     (geometry + XCD-ordered tile lists resident on the device), which the Python autograd
+//     Function and the RCCL data-parallel path compose.
+//
+// No host synchronisation anywhere in these ops: they only enqueue on the current HIP stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+
+#include "ntxent/ntxent.h"
+
+namespace ntxent {
+namespace th {
+
+DType to_dtype(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return DType::F32;
+    case at::kHalf: return DType::F16;
+    case at::kBFloat16: return DType::BF16;
+    default: NTXENT_CHECK(false, std::string("unsupported dtype ") + c10::toString(t));
+  }
+  return DType::F32;
+}
+
+at::ScalarType to_scalar(DType t) {
+  return t == DType::F32 ? at::kFloat : (t == DType::F16 ? at::kHalf : at::kBFloat16);
+}
+
+// Compute-dtype policy. Normalised rows live in [-1, 1], where fp16's 10-bit mantissa beats
+// bf16's 7 bits at equal MFMA rate, so reduced precision means fp16 unless asked otherwise.
+DType choose_compute(at::ScalarType in, bool use_mixed_precision, const std::string& override_) {
+  if (override_ == "fp32" || override_ == "float32") return DType::F32;
+  if (override_ == "fp16" || override_ == "float16") return DType::F16;
+  if (override_ == "bf16" || override_ == "bfloat16") return DType::BF16;
+  NTXENT_CHECK(override_.empty() || override_ == "auto", "compute_dtype must be auto|fp32|fp16|bf16");
+  if (in == at::kFloat && !use_mixed_precision) return DType::F32;
+  return DType::F16;
+}
+
+struct Plan {
+  Geometry g;
+  DType comp = DType::F16;
+  int device = 0;
+  at::Tensor fwd_tiles;  // int32 [n, 4] on device
+  int n_fwd = 0;
+  at::Tensor dz_tiles;
+  int n_dz = 0;
+  int ksplit = 1;
+
+  int rows() const { return g.rows; }
+  int rows_pad() const { return g.rows_pad; }
+  int dim() const { return g.dim; }
+  int dim_k() const { return g.dim_k; }
+  int dim_n() const { return g.dim_n; }
+  int world() const { return g.world; }
+  int rank() const { return g.rank; }
+  int row_tiles() const { return g.row_tiles; }
+  int col_tiles() const { return g.col_tiles; }
+  double temperature() const { return g.temperature; }
+  std::string compute_dtype() const { return dtype_name(comp); }
+};
+
+static at::Tensor upload_tiles(const std::vector<int4>& v, int device) {
+  auto cpu = torch::empty({(long)v.size(), 4}, torch::dtype(torch::kInt32));
+  std::memcpy(cpu.data_ptr<int>(), v.data(), v.size() * sizeof(int4));
+  return cpu.to(torch::Device(torch::kCUDA, device), /*non_blocking=*/false);
+}
+
+std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double temperature,
+                               const std::string& compute, int device) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int, float, int, int>, std::shared_ptr<Plan>> cache;
+  const DType comp = choose_compute(at::kFloat, compute != "fp32" && compute != "float32", compute);
+  auto key = std::make_tuple(rows, dim, world, rank, (float)temperature, (int)comp, device);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  auto p = std::make_shared<Plan>();
+  p->g = make_geometry(rows, dim, world, rank, (float)temperature);
+  p->comp = comp;
+  p->device = device;
+  const DeviceInfo& di = device_info(device);
+  auto ft = build_fwd_tiles(p->g);
+  p->n_fwd = (int)ft.size();
+  p->fwd_tiles = upload_tiles(ft, device);
+  p->ksplit = choose_dz_ksplit(p->g, di.num_cus);
+  auto dt = build_dz_tiles(p->g, p->ksplit);
+  p->n_dz = (int)dt.size();
+  p->dz_tiles = upload_tiles(dt, device);
+  cache.emplace(key, p);
+  return p;
+}
+
+static hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+static void check_input(const at::Tensor& h, const char* name) {
+  NTXENT_CHECK(h.is_cuda(), std::string(name) + " must be a GPU (HIP) tensor");
+  NTXENT_CHECK(h.is_contiguous(), std::string(name) + " must be contiguous");
+}
+
+static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
+  return at::TensorOptions().dtype(t).device(like.device());
+}
+
+// ---- stage ops ----------------------------------------------------------------------
+std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
+  check_input(h, "h");
+  NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
+  const c10::hip::HIPGuard guard(h.device());
+  auto zq = at::empty({P.g.rows_pad, P.g.dim_k}, opts(h, to_scalar(P.comp)));
+  auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
+  auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
+  launch_prep(to_dtype(h.scalar_type()), P.comp, h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(),
+              ypos.data_ptr<float>(), P.g, cur_stream(h));
+  return {zq, inv, ypos};
+}
+
+at::Tensor transpose(const at::Tensor& zq, const Plan& P) {
+  check_input(zq, "zq");
+  const c10::hip::HIPGuard guard(zq.device());
+  auto zqt = at::empty({P.g.dim_n, P.g.rows_pad}, zq.options());
+  launch_transpose(P.comp, zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
+  return zqt;
+}
+
+std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P,
+                                  bool keep_cos) {
+  check_input(zq_local, "zq_local");
+  check_input(zq_all, "zq_all");
+  NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.g.dim_k,
+               "zq_all must be [world*rows_pad, dim_k]");
+  const c10::hip::HIPGuard guard(zq_local.device());
+  auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
+  at::Tensor sc;
+  if (keep_cos)
+    sc = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
+                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
+                   P.g, cur_stream(zq_local));
+  return {part, sc};
+}
+
+// Writes this rank's slice of lse2_all (log2 units); returns the local loss contribution.
+at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, const Plan& P) {
+  check_input(part, "part");
+  NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad && lse2_all.scalar_type() == at::kFloat,
+               "lse2_all must be float32 [world*rows_pad]");
+  const c10::hip::HIPGuard guard(part.device());
+  auto block_loss = at::empty({P.g.rows_pad / 256}, opts(part, at::kFloat));
+  auto loss = at::empty({}, opts(part, at::kFloat));
+  launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(),
+             lse2_all.data_ptr<float>(), block_loss.data_ptr<float>(), loss.data_ptr<float>(), P.g,
+             cur_stream(part));
+  return loss;
+}
+
+void coef(at::Tensor& sc, const at::Tensor& lse2_all, const Plan& P) {
+  check_input(sc, "sc");
+  const c10::hip::HIPGuard guard(sc.device());
+  launch_coef(P.comp, sc.data_ptr(), lse2_all.data_ptr<float>(),
+              reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sc));
+}
+
+at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& lse2_all,
+                     const Plan& P) {
+  check_input(zq_local, "zq_local");
+  const c10::hip::HIPGuard guard(zq_local.device());
+  auto sc = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), sc.data_ptr(), lse2_all.data_ptr<float>(),
+                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g,
+                   cur_stream(zq_local));
+  return sc;
+}
+
+at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
+  check_input(sc, "sc");
+  check_input(zqt_all, "zqt_all");
+  NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.rows_pad, "zqt_all must be [world, dim_n, rows_pad]");
+  const c10::hip::HIPGuard guard(sc.device());
+  auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
+  launch_dz(P.comp, sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
+            P.n_dz, P.ksplit, slabs.data_ptr<float>(), P.g, cur_stream(sc));
+  return slabs;
+}
+
+at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
+                    const Plan& P) {
+  check_input(h, "h");
+  const c10::hip::HIPGuard guard(h.device());
+  auto go = grad_out.to(at::kFloat).contiguous();
+  auto dh = at::empty_like(h);
+  launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), P.ksplit, h.data_ptr(), inv.data_ptr<float>(),
+                  go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
+  return dh;
+}
+
+// ---- single-process fused flows ------------------------------------------------------
+// Returns {loss, zq, zqt, inv, lse2, sc}; `sc` holds cosines (keep_cos) or is undefined.
+std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::string& compute, bool keep_cos) {
+  check_input(h, "h");
+  NTXENT_CHECK(h.dim() == 2, "z must be 2-D [2N, d]");
+  const c10::hip::HIPGuard guard(h.device());
+  const DType comp = choose_compute(h.scalar_type(), compute != "fp32", compute);
+  auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
+  auto pr = prep(h, *P);
+  auto zqt = transpose(pr[0], *P);
+  auto fs = fwd_stats(pr[0], pr[0], *P, keep_cos);
+  auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  auto loss = lse(fs[0], pr[2], lse2, *P);
+  return {loss, pr[0], zqt, pr[1], lse2, fs[1]};
+}
+
+at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const at::Tensor& zqt, const at::Tensor& inv,
+                          const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& grad_out,
+                          double T, const std::string& compute) {
+  const c10::hip::HIPGuard guard(h.device());
+  const DType comp = to_dtype(zq.scalar_type());
+  auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
+  at::Tensor sc;
+  if (sc_in.has_value() && sc_in->defined()) {
+    sc = *sc_in;
+    coef(sc, lse2, *P);
+  } else {
+    sc = coef_gemm(zq, zq, lse2, *P);
+  }
+  auto slabs = dz(sc, zqt, *P);
+  return norm_bwd(slabs, h, inv, grad_out, *P);
+}
+
+// ---- reference-compatible API (src/binding_new.cpp:5-20) -------------------------------
+at::Tensor forward_op(const at::Tensor& z, double T, bool use_mixed_precision) {
+  auto out = fused_forward(z.contiguous(), T, use_mixed_precision ? "fp16" : "auto", /*keep_cos=*/false);
+  return out[0];
+}
+
+std::vector<at::Tensor> forward_with_stats(const at::Tensor& z, double T, bool use_mixed_precision) {
+  auto out = fused_forward(z.contiguous(), T, use_mixed_precision ? "fp16" : "auto", false);
+  const int R = (int)z.size(0);
+  auto lse_nat = out[4].narrow(0, 0, R) * (float)0.6931471805599453;
+  return {out[0], lse_nat};
+}
+
+// backward(z, stats, grad_out, T): `stats` = the natural-log LSE [2N] from forward_with_stats;
+// any other shape (e.g. the reference's [2N,2N] softmax) makes the op recompute the stats.
+// Returns (grad_z, grad_logits) where grad_logits = dL/dS is materialised only for 2N <= 4096.
+std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at::Tensor& stats,
+                                               const at::Tensor& grad_out, double T, bool use_mixed_precision) {
+  auto z = z_in.contiguous();
+  const c10::hip::HIPGuard guard(z.device());
+  const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
+  auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
+  auto pr = prep(z, *P);
+  auto zqt = transpose(pr[0], *P);
+  at::Tensor lse2 = at::zeros({P->g.rows_pad}, opts(z, at::kFloat));
+  if (stats.dim() == 1 && stats.numel() == z.size(0)) {
+    lse2.narrow(0, 0, z.size(0)).copy_(stats.to(at::kFloat) * (float)1.4426950408889634);
+  } else {
+    auto fs = fwd_stats(pr[0], pr[0], *P, false);
+    lse(fs[0], pr[2], lse2, *P);
+  }
+  auto sc = coef_gemm(pr[0], pr[0], lse2, *P);
+  auto slabs = dz(sc, zqt, *P);
+  auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
+  auto dh = norm_bwd(slabs, z, pr[1], go, *P);
+  at::Tensor grad_logits;
+  if (z.size(0) <= 4096) {
+    // dL/dS_ij = grad_out * (P_ij - [j == p(i)]) / 2N  (debug/parity output)
+    const long R = z.size(0), n = R / 2;
+    auto zf = z.to(at::kFloat);
+    auto zn = zf / zf.norm(2, {1}, true).clamp_min(1e-12);
+    auto S = at::matmul(zn, zn.t()) / T;
+    S.fill_diagonal_(-std::numeric_limits<float>::infinity());
+    auto lse_nat = lse2.narrow(0, 0, R) * (float)0.6931471805599453;
+    auto G = at::exp(S - lse_nat.unsqueeze(1));
+    auto idx = at::arange(R, opts(z, at::kLong));
+    auto pos = (idx + n) % R;
+    G.index_put_({idx, pos}, G.index({idx, pos}) - 1.0);
+    grad_logits = G * (go / (double)R);
+  } else {
+    grad_logits = at::empty({0}, opts(z, at::kFloat));
+  }
+  return {dh, grad_logits};
+}
+
+bool check_tensor_core_support() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  return check_matrix_core_support(dev);
+}
+
+}  // namespace th
+}  // namespace ntxent
+
+// ---- torch.ops registration (python/test.py:137 resolves `torch.ops.ntxent_cuda`) -------
+TORCH_LIBRARY(ntxent_cuda, m) {
+  m.def("forward(Tensor z, float T, bool use_mixed_precision=False) -> Tensor");
+  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False) -> (Tensor, Tensor)");
+  m.def("check_tensor_core_support() -> bool", &ntxent::th::check_tensor_core_support);
+}
+TORCH_LIBRARY_IMPL(ntxent_cuda, CUDA, m) {
+  m.impl("forward", &ntxent::th::forward_op);
+  m.impl("backward", &ntxent::th::backward_op);
+}
+TORCH_LIBRARY(ntxent, m) {
+  m.def("forward(Tensor z, float T, bool use_mixed_precision=False) -> Tensor");
+  m.def("forward_with_stats(Tensor z, float T, bool use_mixed_precision=False) -> Tensor[]");
+  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False) -> (Tensor, Tensor)");
+}
+TORCH_LIBRARY_IMPL(ntxent, CUDA, m) {
+  m.impl("forward", &ntxent::th::forward_op);
+  m.impl("forward_with_stats", &ntxent::th::forward_with_stats);
+  m.impl("backward", &ntxent::th::backward_op);
+}
+
+// ---- pybind11 module ---------------------------------------------------------------------
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  namespace py = pybind11;
+  using namespace ntxent::th;
+  m.doc() = "MI355X (gfx950) NT-Xent loss: MFMA/LDS HIP kernels";
+  py::class_<Plan, std::shared_ptr<Plan>>(m, "Plan")
+      .def_property_readonly("rows", &Plan::rows)
+      .def_property_readonly("rows_pad", &Plan::rows_pad)
+      .def_property_readonly("dim", &Plan::dim)
+      .def_property_readonly("dim_k", &Plan::dim_k)
+      .def_property_readonly("dim_n", &Plan::dim_n)
+      .def_property_readonly("world", &Plan::world)
+      .def_property_readonly("rank", &Plan::rank)
+      .def_property_readonly("row_tiles", &Plan::row_tiles)
+      .def_property_readonly("col_tiles", &Plan::col_tiles)
+      .def_property_readonly("temperature", &Plan::temperature)
+      .def_property_readonly("compute_dtype", &Plan::compute_dtype)
+      .def_readonly("n_fwd_tiles", &Plan::n_fwd)
+      .def_readonly("n_dz_tiles", &Plan::n_dz)
+      .def_readonly("ksplit", &Plan::ksplit)
+      .def_readonly("fwd_tiles", &Plan::fwd_tiles)
+      .def_readonly("dz_tiles", &Plan::dz_tiles);
+  m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
+        py::arg("temperature"), py::arg("compute"), py::arg("device"));
+  m.def("choose_compute", [](const std::string& in_dtype, bool mp, const std::string& ov) {
+    at::ScalarType t = in_dtype == "float32" ? at::kFloat : (in_dtype == "float16" ? at::kHalf : at::kBFloat16);
+    return std::string(ntxent::dtype_name(choose_compute(t, mp, ov)));
+  });
+  m.def("prep", &prep);
+  m.def("transpose", &transpose);
+  m.def("fwd_stats", &fwd_stats);
+  m.def("lse", &lse);
+  m.def("coef", &coef);
+  m.def("coef_gemm", &coef_gemm);
+  m.def("dz", &dz);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
+        py::arg("keep_cos") = true);
+  m.def("fused_backward", &fused_backward);
+  // reference API names and kwargs
+  m.def("forward", &forward_op, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
+  m.def("forward_with_stats", &forward_with_stats, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
+  m.def("backward", &backward_op, py::arg("z"), py::arg("softmax"), py::arg("grad_out"), py::arg("T"),
+        py::arg("use_mixed_precision") = false);
+  m.def("check_tensor_core_support", &check_tensor_core_support);
+  m.def("check_matrix_core_support", &check_tensor_core_support);
+  m.def("get_optimal_block_size", &ntxent::get_optimal_block_size);
+  m.def("device_info", [](int dev) {
+    const auto& d = ntxent::device_info(dev);
+    py::dict r;
+    r["device"] = d.device;
+    r["num_cus"] = d.num_cus;
+    r["lds_per_block"] = d.lds_per_block;
+    r["warp_size"] = d.warp_size;
+    r["arch"] = d.arch;
+    r["is_gfx950"] = d.is_gfx950;
+    return r;
+  });
+  m.attr("TILE") = ntxent::kTile;
+}

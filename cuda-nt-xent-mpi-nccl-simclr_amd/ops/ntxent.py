@@ -1,0 +1,145 @@
+"""NT-Xent loss on MI355X: autograd Function, functional API and ``nn.Module``.
+
+The reference exposes raw ``forward``/``backward`` ops with no autograd link
+(``src/binding_new.cpp:4-21``); its tests nevertheless call ``loss.backward()``
+(``tests/test_forward.cpp:29-38``). Here the HIP kernels are wrapped in a
+``torch.autograd.Function`` so that works, and the backward honours ``grad_out``.
+
+Execution (single process; see ``parallel.distributed`` for global-batch negatives):
+  forward : prep (L2-normalise, quantise to the compute dtype, positive logits)
+            -> fused MFMA similarity GEMM with per-tile online LSE partials (upper-triangular
+               tiles only, S is symmetric) -> LSE merge + deterministic loss reduction
+  backward: coefficient pass C = P + P^T - 2 I_pos (in place over the kept cosines, or
+            recomputed by the GEMM when ``keep_logits=False``) -> MFMA dZ = C Z
+            -> fused grad_out/(2N tau) scale + L2-normalisation backward.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import _ext, reference
+
+_VALID_COMPUTE = ("auto", "fp32", "fp16", "bf16")
+
+
+def _use_reference(h: torch.Tensor) -> bool:
+    if not h.is_cuda:
+        return True
+    return os.environ.get("NTXENT_FORCE_REFERENCE", "0") == "1"
+
+
+def resolve_compute(dtype: torch.dtype, use_mixed_precision: bool = False, compute: str = "auto") -> str:
+    """Compute-dtype policy (mirrors the C++ one): fp32 inputs stay exact fp32 unless
+    mixed precision is requested; reduced precision is fp16 (normalised rows in [-1, 1])."""
+    if compute not in _VALID_COMPUTE:
+        raise ValueError(f"compute must be one of {_VALID_COMPUTE}")
+    if compute != "auto":
+        return compute
+    if dtype == torch.float32 and not use_mixed_precision:
+        return "fp32"
+    return "fp16"
+
+
+class NTXentFunction(torch.autograd.Function):
+    """loss = NTXent(h) for stacked views h = [h1; h2] on one GPU."""
+
+    @staticmethod
+    def forward(ctx, h: torch.Tensor, temperature: float, compute: str, keep_logits: bool):
+        C = _ext.load()
+        h = h.contiguous()
+        loss, zq, zqt, inv, lse2, sc = C.fused_forward(h, float(temperature), compute, bool(keep_logits))
+        ctx.temperature = float(temperature)
+        ctx.compute = compute
+        ctx.sc = sc if keep_logits else None  # consumed (overwritten) by the first backward
+        ctx.save_for_backward(h, zq, zqt, inv, lse2)
+        ctx.mark_non_differentiable()
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out: torch.Tensor):
+        C = _ext.load()
+        h, zq, zqt, inv, lse2 = ctx.saved_tensors
+        sc, ctx.sc = ctx.sc, None  # a second backward (retain_graph) recomputes the cosines
+        dh = C.fused_backward(h, zq, zqt, inv, lse2, sc, grad_out.reshape(1), ctx.temperature, ctx.compute)
+        return dh, None, None, None
+
+
+def ntxent_loss(h: torch.Tensor, temperature: float = 0.07, *, use_mixed_precision: bool = False,
+                compute: str = "auto", keep_logits: bool = True, z2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NT-Xent loss of stacked views ``h = [h1; h2]`` (or ``h1=h, z2=h2``).
+
+    Args:
+      temperature: tau.
+      use_mixed_precision: fp32 inputs are computed in fp16 (fp32 accumulate) if True.
+      compute: override the compute dtype: ``auto|fp32|fp16|bf16``.
+      keep_logits: keep the cosine tiles (compute dtype) between forward and backward
+        (default; saves one similarity GEMM). False recomputes them in the backward.
+    """
+    if z2 is not None:
+        h = torch.cat([h, z2], 0)
+    if h.dim() != 2 or h.shape[0] % 2:
+        raise ValueError("expected stacked views [2N, d]")
+    if _use_reference(h):
+        if h.is_cuda and os.environ.get("NTXENT_ALLOW_REFERENCE", "0") != "1":
+            raise RuntimeError("NTXENT_FORCE_REFERENCE requires NTXENT_ALLOW_REFERENCE=1")
+        return reference.ntxent_loss(h, temperature)
+    comp = resolve_compute(h.dtype, use_mixed_precision, compute)
+    return NTXentFunction.apply(h, float(temperature), comp, bool(keep_logits))
+
+
+class NTXentLoss(torch.nn.Module):
+    """``nn.Module`` front end: ``NTXentLoss(temperature)(z1, z2)`` or ``(h)``.
+
+    With ``distributed=True`` negatives come from the whole data-parallel group (RCCL
+    all-gather over xGMI), see :mod:`parallel.distributed`.
+    """
+
+    def __init__(self, temperature: float = 0.07, use_mixed_precision: bool = False, compute: str = "auto",
+                 keep_logits: bool = True, distributed: bool = False, group=None):
+        super().__init__()
+        self.temperature = float(temperature)
+        self.use_mixed_precision = use_mixed_precision
+        self.compute = compute
+        self.keep_logits = keep_logits
+        self.distributed = distributed
+        self.group = group
+
+    def forward(self, z1: torch.Tensor, z2: Optional[torch.Tensor] = None) -> torch.Tensor:
+        h = z1 if z2 is None else torch.cat([z1, z2], 0)
+        if self.distributed:
+            from ..parallel.distributed import dist_ntxent_loss
+
+            return dist_ntxent_loss(h, self.temperature, group=self.group, compute=self.compute,
+                                    use_mixed_precision=self.use_mixed_precision, keep_logits=self.keep_logits)
+        return ntxent_loss(h, self.temperature, use_mixed_precision=self.use_mixed_precision,
+                           compute=self.compute, keep_logits=self.keep_logits)
+
+    def extra_repr(self) -> str:
+        return f"temperature={self.temperature}, compute={self.compute}, distributed={self.distributed}"
+
+
+# ---- reference-compatible raw op API (src/binding_new.cpp:5-20) --------------------------
+def forward(z: torch.Tensor, T: float, use_mixed_precision: bool = False) -> torch.Tensor:
+    return _ext.load().forward(z, float(T), use_mixed_precision)
+
+
+def forward_with_stats(z: torch.Tensor, T: float, use_mixed_precision: bool = False):
+    return tuple(_ext.load().forward_with_stats(z, float(T), use_mixed_precision))
+
+
+def backward(z: torch.Tensor, softmax: torch.Tensor, grad_out: torch.Tensor, T: float,
+             use_mixed_precision: bool = False):
+    return tuple(_ext.load().backward(z, softmax, grad_out, float(T), use_mixed_precision))
+
+
+def check_tensor_core_support() -> bool:
+    try:
+        return bool(_ext.load(build_if_missing=False).check_tensor_core_support())
+    except Exception:
+        return False
+
+
+check_matrix_core_support = check_tensor_core_support

@@ -1,0 +1,176 @@
+"""HIP kernel numerics vs the PyTorch fp64 oracle (run on an MI355X).
+
+Covers the intents of the reference's GTest/pytest suites (tests/test_forward.cpp,
+tests/test_backward.cpp, python/test.py) with value checks they never had.
+"""
+import math
+
+import pytest
+import torch
+
+from ntxent_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+
+TOL = {  # (loss rtol, grad max-abs err relative to max |grad|)
+    "fp32": (2e-5, 2e-4),
+    "fp16": (3e-3, 2e-2),
+    "bf16": (1.5e-2, 6e-2),
+}
+
+
+def _inputs(rows, dim, dtype, seed=0, noise=0.3):
+    g = torch.Generator().manual_seed(seed)
+    n = rows // 2
+    base = torch.randn(n, dim, generator=g, dtype=torch.float64)
+    v1 = base + noise * torch.randn(n, dim, generator=g, dtype=torch.float64)
+    v2 = base + noise * torch.randn(n, dim, generator=g, dtype=torch.float64)
+    h64 = torch.cat([v1, v2], 0)
+    return h64, h64.to(dtype).cuda()
+
+
+def _oracle(h_dev, T):
+    h = h_dev.detach().double().cpu().requires_grad_(True)
+    loss = R.ntxent_loss(h, T)
+    (g,) = torch.autograd.grad(loss, h)
+    return loss.item(), g
+
+
+def _check(h_dev, T, compute, keep=True):
+    import ntxent_amd
+
+    x = h_dev.clone().requires_grad_(True)
+    loss = ntxent_amd.ntxent_loss(x, T, compute=compute, keep_logits=keep)
+    (g,) = torch.autograd.grad(loss, x)
+    lref, gref = _oracle(h_dev, T)
+    lt, gt = TOL[compute]
+    assert math.isfinite(loss.item())
+    assert abs(loss.item() - lref) <= lt * max(1.0, abs(lref)), (loss.item(), lref)
+    err = (g.double().cpu() - gref).abs().max().item()
+    scale = gref.abs().max().item()
+    assert err <= gt * scale, (err, scale)
+    return loss.item(), lref, err / scale
+
+
+@pytest.mark.parametrize("compute", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("rows,dim", [(64, 128), (34, 100), (512, 256), (600, 200), (1024, 512)])
+def test_fwd_bwd_matches_oracle(ext, rows, dim, compute):
+    _, h = _inputs(rows, dim, torch.float32, seed=rows + dim)
+    _check(h, 0.07, compute)
+
+
+@pytest.mark.parametrize("in_dtype", [torch.bfloat16, torch.float16])
+def test_low_precision_inputs(ext, in_dtype):
+    _, h = _inputs(768, 384, in_dtype, seed=7)
+    _check(h, 0.1, "fp16")
+
+
+@pytest.mark.parametrize("rows,dim", [(512, 256), (1030, 96)])
+def test_recompute_equals_store(ext, rows, dim):
+    import ntxent_amd
+
+    _, h = _inputs(rows, dim, torch.float32, seed=3)
+    out = []
+    for keep in (True, False):
+        x = h.clone().requires_grad_(True)
+        loss = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16", keep_logits=keep)
+        (g,) = torch.autograd.grad(loss, x)
+        out.append((loss.item(), g))
+    assert out[0][0] == out[1][0]
+    assert torch.allclose(out[0][1], out[1][1], rtol=1e-2, atol=1e-6 * out[0][1].abs().max().item() + 1e-9)
+
+
+def test_grad_out_scaling(ext):
+    import ntxent_amd
+
+    _, h = _inputs(256, 64, torch.float32, seed=5)
+    x = h.clone().requires_grad_(True)
+    loss = ntxent_amd.ntxent_loss(x, 0.5, compute="fp32")
+    (3.5 * loss).backward()
+    _, gref = _oracle(h, 0.5)
+    assert torch.allclose(x.grad.double().cpu(), 3.5 * gref, rtol=1e-3, atol=1e-7)
+
+
+@pytest.mark.parametrize("scale", [1e-5, 1.0, 1e5])
+@pytest.mark.parametrize("T", [0.01, 0.07, 1.0])
+def test_numerical_stability_grid(ext, scale, T):
+    """The reference harness's stability grid (python/test.py:57-79) with value checks."""
+    import ntxent_amd
+
+    g = torch.Generator().manual_seed(11)
+    z = torch.nn.functional.normalize(torch.randn(256, 256, generator=g), dim=1) * scale
+    x = z.cuda().requires_grad_(True)
+    loss = ntxent_amd.ntxent_loss(x, T, compute="fp32")
+    (gr,) = torch.autograd.grad(loss, x)
+    assert torch.isfinite(loss) and torch.isfinite(gr).all()
+    lref, gref = _oracle(z.cuda(), T)
+    assert abs(loss.item() - lref) <= 1e-4 * max(1.0, abs(lref))
+    assert (gr.double().cpu() - gref).abs().max() <= 1e-3 * gref.abs().max() + 1e-12
+
+
+def test_zero_rows_are_finite(ext):
+    import ntxent_amd
+
+    _, h = _inputs(128, 64, torch.float32)
+    h[3] = 0
+    x = h.clone().requires_grad_(True)
+    loss = ntxent_amd.ntxent_loss(x, 0.07, compute="fp32")
+    (g,) = torch.autograd.grad(loss, x)
+    assert torch.isfinite(loss) and torch.isfinite(g).all()
+
+
+def test_deterministic(ext):
+    import ntxent_amd
+
+    _, h = _inputs(1024, 256, torch.bfloat16, seed=9)
+    res = []
+    for _ in range(3):
+        x = h.clone().requires_grad_(True)
+        loss = ntxent_amd.ntxent_loss(x, 0.07)
+        (g,) = torch.autograd.grad(loss, x)
+        res.append((loss.item(), g))
+    for l, g in res[1:]:
+        assert l == res[0][0]
+        assert torch.equal(g, res[0][1])
+
+
+def test_reference_api_forward_backward(ext):
+    """forward / forward_with_stats / backward with the reference's names and kwargs."""
+    _, h = _inputs(64, 128, torch.float32, seed=1)
+    loss = ext.forward(h, 0.07)
+    loss2, lse = ext.forward_with_stats(h, 0.07, use_mixed_precision=False)
+    lref, lse_ref, _ = R.ntxent_stats(h.double().cpu(), 0.07)
+    assert abs(loss.item() - lref.item()) < 1e-4
+    assert torch.allclose(lse.double().cpu(), lse_ref, atol=1e-4)
+    go = torch.tensor(1.0, device=h.device)
+    gz, glog = ext.backward(h, lse, go, 0.07)
+    gref = R.ntxent_backward_analytic(h.double().cpu(), 0.07)
+    assert (gz.double().cpu() - gref).abs().max() < 1e-4 * gref.abs().max() + 1e-9
+    assert glog.shape == (64, 64)
+    gz2, _ = torch.ops.ntxent_cuda.backward(h, torch.empty(64, 64, device=h.device), go, 0.07)
+    assert torch.allclose(gz, gz2, atol=1e-6)
+    assert torch.ops.ntxent_cuda.forward(h, 0.07).item() == pytest.approx(loss.item(), rel=1e-6)
+    assert ext.check_tensor_core_support() is True
+
+
+@pytest.mark.parametrize("B", [16, 32, 64, 128])
+def test_different_batch_sizes(ext, B):
+    """tests/test_forward.cpp:41-51 DifferentBatchSizes, with an oracle value check."""
+    _, h = _inputs(2 * B, 128, torch.float32, seed=B)
+    _check(h, 0.07, "fp32")
+
+
+def test_no_quadratic_fp32_buffer(ext):
+    """Peak memory stays far below one fp32 (2N)^2 logits matrix."""
+    import ntxent_amd
+
+    _, h = _inputs(8192, 256, torch.bfloat16, seed=2)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    x = h.clone().requires_grad_(True)
+    loss = ntxent_amd.ntxent_loss(x, 0.07)
+    (g,) = torch.autograd.grad(loss, x)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert peak < 8192 * 8192 * 4 * 0.9, peak  # below one fp32 logits matrix

@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""In-tree native build for ntxent-mi355x (gfx950 only).
+
+Drives hipcc directly — no hipify pass, no torch JIT cache — and drops the extension
+next to the Python package so it travels with the repo snapshot to the GPU box:
+
+  <pkg>/_C.<abi>.so            PyTorch extension (pybind11 + TORCH_LIBRARY)
+  build/bin/ntxent_bench       C++ benchmark (reference src/benchmark.cpp)
+  build/bin/ntxent_tests       C++ tests    (reference tests/test_*.cpp)
+
+Incremental: an object is rebuilt only when a source or header it depends on is newer.
+Usage: python tools/build_ext.py [--force] [--no-cpp] [-v]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+PKG = ROOT / "cuda-nt-xent-mpi-nccl-simclr_amd"
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build"
+ARCH = os.environ.get("NTXENT_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    inc = [str(p) for p in ce.include_paths()]
+    libdir = str(Path(torch.__file__).parent / "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, libdir, abi
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def ext_path() -> Path:
+    return PKG / f"_C{ext_suffix()}"
+
+
+def _headers():
+    return list((CSRC / "include").rglob("*.h")) + list((CSRC / "kernels").glob("*.h"))
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[-1] if cmd else cmd}")
+    return r
+
+
+def build(force: bool = False, cpp_targets: bool = True, verbose: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    (BUILD / "bin").mkdir(exist_ok=True)
+    tinc, tlib, abi = _torch_paths()
+    pyinc = sysconfig.get_paths()["include"]
+    common = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}"]
+    hdrs = _headers()
+
+    k_src = CSRC / "kernels" / "ntxent_kernels.hip"
+    k_obj = BUILD / "ntxent_kernels.o"
+    t_src = CSRC / "runtime" / "ntxent_torch.cpp"
+    t_obj = BUILD / "ntxent_torch.o"
+    jobs = []
+    if force or _stale(k_obj, [k_src, *hdrs]):
+        jobs.append(common + ["-O3", "-c", str(k_src), "-o", str(k_obj)])
+    if force or _stale(t_obj, [t_src, *hdrs]):
+        tflags = [f"-I{p}" for p in tinc] + [
+            f"-I{pyinc}",
+            "-O2",
+            "-DTORCH_EXTENSION_NAME=_C",
+            "-DTORCH_API_INCLUDE_EXTENSION_H",
+            f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+            "-DUSE_ROCM=1",
+            "-Wno-unused-result",
+            "-Wno-deprecated-declarations",
+        ]
+        # host-only translation unit: compile as plain C++ (no device pass over libtorch headers)
+        hostc = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-std=c++17", "-fPIC", "-I/opt/rocm/include", f"-I{CSRC / 'include'}"]
+        jobs.append(hostc + tflags + ["-c", str(t_src), "-o", str(t_obj)])
+    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+
+    so = ext_path()
+    if force or _stale(so, [k_obj, t_obj]):
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(k_obj), str(t_obj), "-o", str(so),
+                f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+                f"-Wl,-rpath,{tlib}"]
+        _run(link, verbose)
+
+    if cpp_targets:
+        build_cpp_targets(k_obj, force=force, verbose=verbose)
+    return so
+
+
+def build_cpp_targets(k_obj: Path, force: bool = False, verbose: bool = False):
+    """Standalone C++ executables (no libtorch): benchmark + tests over the raw API."""
+    hdrs = _headers()
+    targets = {
+        "ntxent_bench": ROOT / "bench" / "ntxent_bench.cpp",
+        "ntxent_tests": ROOT / "tests" / "cpp" / "ntxent_tests.cpp",
+    }
+    jobs = []
+    for name, src in targets.items():
+        if not src.exists():
+            continue
+        out = BUILD / "bin" / name
+        if force or _stale(out, [src, k_obj, *hdrs]):
+            jobs.append([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O2", f"-I{CSRC / 'include'}",
+                         str(src), str(k_obj), "-o", str(out)])
+    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--no-cpp", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    so = build(force=a.force, cpp_targets=not a.no_cpp, verbose=a.verbose)
+    print(f"built {so.relative_to(ROOT)}")
+
+
+if __name__ == "__main__":
+    main()
