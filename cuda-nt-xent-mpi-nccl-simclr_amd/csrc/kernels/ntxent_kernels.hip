@@ -43,7 +43,9 @@ struct SimParams {
   float y_scale;         // inv_temp * log2(e)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
   char* sc;              // tile-blocked cosine / coefficient buffer
-  const float* lse2;     // [W*Rpad] lse in log2 units
+  const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
+  const float* ypos;     // [R] positive logit (log2 units, from the quantised rows)
+  const float* lseneg2;  // [Rpad] log2-sum-exp2 over the NEGATIVES of each local row
   float* out;            // dZ slabs
   long long ldo;         // elements
   long long slab_stride; // elements
@@ -85,12 +87,19 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt
       const bool rvalid = gi < p.R;
       const float lrow = p.lse2[p.own0 + gi];
       const int gself = p.own0 + gi;
-      const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
+      const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
+      const int gpos = p.own0 + lpos;
+      // positive: P_ip - 1 = -sigmoid(lse_neg_i - y_ip) (no 1 - P cancellation when P ~ 1)
+      float cpos = 0.f;
+      if (rvalid) {
+        const float yp = p.ypos[gi];
+        cpos = -(1.0f / (1.0f + fast_exp2(yp - p.lseneg2[gi])) + 1.0f / (1.0f + fast_exp2(yp - p.lseneg2[lpos])));
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const float y = acc[mi][ni][r] * p.y_scale;
         float v = fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
-        v = (gj[ni] == gpos) ? v - 2.0f : v;
+        v = (gj[ni] == gpos) ? cpos : v;
         v = (rvalid && cvalid[ni] && gj[ni] != gself) ? v : 0.0f;
         c[ni][r] = v;
       }
@@ -244,21 +253,28 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           }
         }
     }
-    // masks -> scaled logits in log2 units (-inf where excluded)
+    // masks -> scaled logits in log2 units (-inf where excluded). The partials cover the
+    // NEGATIVES only: self and positive are excluded (the positive logit comes from prep), so
+    // the loss is softplus(lse_neg - y_pos) with no lse - y cancellation.
     const int col_local0 = (nt * kTile) % p.Rpad;
+    const bool own_blk = kind != kTilePlain;
     bool cvalid[4];
+    int cloc[4];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) cvalid[ni] = (col_local0 + 64 * wn + 16 * ni + (lane & 15)) < p.R;
+    for (int ni = 0; ni < 4; ++ni) {
+      cloc[ni] = col_local0 + 64 * wn + 16 * ni + (lane & 15);
+      cvalid[ni] = cloc[ni] < p.R;
+    }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row_t = 128 * wm + 16 * mi + 4 * (lane >> 4) + r;
-        const bool rvalid = mt * kTile + row_t < p.R;
+        const int gi = mt * kTile + 128 * wm + 16 * mi + 4 * (lane >> 4) + r;
+        const bool rvalid = gi < p.R;
+        const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          const int col_t = 64 * wn + 16 * ni + (lane & 15);
-          const bool ok = rvalid && cvalid[ni] && !(kind == kTileDiag && row_t == col_t);
+          const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
           acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
         }
       }
@@ -449,8 +465,8 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
 }
 
 __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ part, const float* __restrict__ ypos,
-                                                  float* __restrict__ lse2_all, float* __restrict__ block_loss,
-                                                  int R, int Rpad, int Tc, int own0) {
+                                                  float* __restrict__ lse2_all, float* __restrict__ lseneg2,
+                                                  float* __restrict__ block_loss, int R, int Rpad, int Tc, int own0) {
   __shared__ float red[16];
   const int i = blockIdx.x * 256 + threadIdx.x;
   float m = kNegInf, s = 0.f;
@@ -459,9 +475,16 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
     lse_merge(m, s, v.x, v.y);
   }
   const bool ok = i < R;
-  const float l2 = m + fast_log2(s);
+  const float yp = ok ? ypos[i] : 0.f;
+  const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
+  // lse = logaddexp(lse_neg, y_pos); loss_i = softplus(lse_neg - y_pos) (natural log)
+  const float mx = fmaxf(neg2, yp);
+  const float l2 = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
   lse2_all[own0 + i] = ok ? l2 : 0.f;
-  const float li = ok ? (l2 - ypos[i]) * kLn2 : 0.f;
+  lseneg2[i] = ok ? neg2 : 0.f;
+  const float x = (neg2 - yp) * kLn2;
+  const float sp = x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
+  const float li = ok ? sp : 0.f;
   const float tot = block_sum(li, red);
   if (threadIdx.x == 0) block_loss[blockIdx.x] = tot;
 }
@@ -648,8 +671,8 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
 }
 
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* sc,
-                      const float* lse2_all, const int4* tiles, int ntiles, const Geometry& g,
-                      hipStream_t stream) {
+                      const float* lse2_all, const float* ypos, const float* lseneg2, const int4* tiles,
+                      int ntiles, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   const long long kb = (long long)g.dim_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
@@ -659,6 +682,8 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   p.kbytes = kb;
   p.sc = static_cast<char*>(sc);
   p.lse2 = lse2_all;
+  p.ypos = ypos;
+  p.lseneg2 = lseneg2;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeCoef>), dim3(ntiles), dim3(kGemmThreads), 0,
@@ -667,10 +692,10 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* block_loss,
+void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* lseneg2, float* block_loss,
                 float* loss_sum, const Geometry& g, hipStream_t stream) {
   const int nb = g.rows_pad / 256;
-  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, block_loss,
+  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, lseneg2, block_loss,
                      g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad);
   NTXENT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(dev::loss_final_kernel, dim3(1), dim3(64), 0, stream, block_loss, nb,
@@ -678,13 +703,15 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* b
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_coef(DType comp, void* sc, const float* lse2_all, const int4* tiles, int ntiles,
-                 const Geometry& g, hipStream_t stream) {
+void launch_coef(DType comp, void* sc, const float* lse2_all, const float* ypos, const float* lseneg2,
+                 const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
   p.tiles = tiles;
   p.sc = static_cast<char*>(sc);
   p.lse2 = lse2_all;
+  p.ypos = ypos;
+  p.lseneg2 = lseneg2;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(ntiles), dim3(kGemmThreads), 0, stream, p);

@@ -11,8 +11,8 @@
 //
 // No host synchronisation anywhere in these ops: they only enqueue on the current HIP stream.
 #include <torch/extension.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include <map>
 #include <memory>
@@ -104,7 +104,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
 }
 
 static hipStream_t cur_stream(const at::Tensor& t) {
-  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 static void check_input(const at::Tensor& h, const char* name) {
@@ -120,7 +120,7 @@ static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
 std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
-  const c10::hip::HIPGuard guard(h.device());
+  const at::DeviceGuard guard(h.device());
   auto zq = at::empty({P.g.rows_pad, P.g.dim_k}, opts(h, to_scalar(P.comp)));
   auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
   auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
@@ -131,7 +131,7 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
 
 at::Tensor transpose(const at::Tensor& zq, const Plan& P) {
   check_input(zq, "zq");
-  const c10::hip::HIPGuard guard(zq.device());
+  const at::DeviceGuard guard(zq.device());
   auto zqt = at::empty({P.g.dim_n, P.g.rows_pad}, zq.options());
   launch_transpose(P.comp, zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
@@ -143,7 +143,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   check_input(zq_all, "zq_all");
   NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.g.dim_k,
                "zq_all must be [world*rows_pad, dim_k]");
-  const c10::hip::HIPGuard guard(zq_local.device());
+  const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
   if (keep_cos)
@@ -155,35 +155,40 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   return {part, sc};
 }
 
-// Writes this rank's slice of lse2_all (log2 units); returns the local loss contribution.
-at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, const Plan& P) {
+// Writes this rank's slice of lse2_all (log2 units) and lseneg2 (negatives-only LSE of the
+// local rows); returns the local loss contribution.
+at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, at::Tensor& lseneg2,
+               const Plan& P) {
   check_input(part, "part");
   NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad && lse2_all.scalar_type() == at::kFloat,
                "lse2_all must be float32 [world*rows_pad]");
-  const c10::hip::HIPGuard guard(part.device());
+  NTXENT_CHECK(lseneg2.numel() == P.g.rows_pad && lseneg2.scalar_type() == at::kFloat,
+               "lseneg2 must be float32 [rows_pad]");
+  const at::DeviceGuard guard(part.device());
   auto block_loss = at::empty({P.g.rows_pad / 256}, opts(part, at::kFloat));
   auto loss = at::empty({}, opts(part, at::kFloat));
   launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(),
-             lse2_all.data_ptr<float>(), block_loss.data_ptr<float>(), loss.data_ptr<float>(), P.g,
-             cur_stream(part));
+             lse2_all.data_ptr<float>(), lseneg2.data_ptr<float>(), block_loss.data_ptr<float>(),
+             loss.data_ptr<float>(), P.g, cur_stream(part));
   return loss;
 }
 
-void coef(at::Tensor& sc, const at::Tensor& lse2_all, const Plan& P) {
+void coef(at::Tensor& sc, const at::Tensor& lse2_all, const at::Tensor& ypos, const at::Tensor& lseneg2,
+          const Plan& P) {
   check_input(sc, "sc");
-  const c10::hip::HIPGuard guard(sc.device());
-  launch_coef(P.comp, sc.data_ptr(), lse2_all.data_ptr<float>(),
+  const at::DeviceGuard guard(sc.device());
+  launch_coef(P.comp, sc.data_ptr(), lse2_all.data_ptr<float>(), ypos.data_ptr<float>(), lseneg2.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sc));
 }
 
 at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& lse2_all,
-                     const Plan& P) {
+                     const at::Tensor& ypos, const at::Tensor& lseneg2, const Plan& P) {
   check_input(zq_local, "zq_local");
-  const c10::hip::HIPGuard guard(zq_local.device());
+  const at::DeviceGuard guard(zq_local.device());
   auto sc = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), sc.data_ptr(), lse2_all.data_ptr<float>(),
-                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g,
-                   cur_stream(zq_local));
+                   ypos.data_ptr<float>(), lseneg2.data_ptr<float>(),
+                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(zq_local));
   return sc;
 }
 
@@ -191,7 +196,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   check_input(sc, "sc");
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.rows_pad, "zqt_all must be [world, dim_n, rows_pad]");
-  const c10::hip::HIPGuard guard(sc.device());
+  const at::DeviceGuard guard(sc.device());
   auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
   launch_dz(P.comp, sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, P.ksplit, slabs.data_ptr<float>(), P.g, cur_stream(sc));
@@ -201,7 +206,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
 at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
                     const Plan& P) {
   check_input(h, "h");
-  const c10::hip::HIPGuard guard(h.device());
+  const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
   launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), P.ksplit, h.data_ptr(), inv.data_ptr<float>(),
@@ -210,33 +215,35 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
 }
 
 // ---- single-process fused flows ------------------------------------------------------
-// Returns {loss, zq, zqt, inv, lse2, sc}; `sc` holds cosines (keep_cos) or is undefined.
+// Returns {loss, zq, zqt, inv, lse2, sc, ypos, lseneg2}; `sc` holds cosines (keep_cos) or is
+// undefined.
 std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::string& compute, bool keep_cos) {
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2, "z must be 2-D [2N, d]");
-  const c10::hip::HIPGuard guard(h.device());
+  const at::DeviceGuard guard(h.device());
   const DType comp = choose_compute(h.scalar_type(), compute != "fp32", compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
   auto pr = prep(h, *P);
   auto zqt = transpose(pr[0], *P);
   auto fs = fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-  auto loss = lse(fs[0], pr[2], lse2, *P);
-  return {loss, pr[0], zqt, pr[1], lse2, fs[1]};
+  auto lseneg2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  auto loss = lse(fs[0], pr[2], lse2, lseneg2, *P);
+  return {loss, pr[0], zqt, pr[1], lse2, fs[1], pr[2], lseneg2};
 }
 
 at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const at::Tensor& zqt, const at::Tensor& inv,
-                          const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& grad_out,
-                          double T, const std::string& compute) {
-  const c10::hip::HIPGuard guard(h.device());
+                          const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& ypos,
+                          const at::Tensor& lseneg2, const at::Tensor& grad_out, double T) {
+  const at::DeviceGuard guard(h.device());
   const DType comp = to_dtype(zq.scalar_type());
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
   at::Tensor sc;
   if (sc_in.has_value() && sc_in->defined()) {
     sc = *sc_in;
-    coef(sc, lse2, *P);
+    coef(sc, lse2, ypos, lseneg2, *P);
   } else {
-    sc = coef_gemm(zq, zq, lse2, *P);
+    sc = coef_gemm(zq, zq, lse2, ypos, lseneg2, *P);
   }
   auto slabs = dz(sc, zqt, *P);
   return norm_bwd(slabs, h, inv, grad_out, *P);
@@ -255,25 +262,25 @@ std::vector<at::Tensor> forward_with_stats(const at::Tensor& z, double T, bool u
   return {out[0], lse_nat};
 }
 
-// backward(z, stats, grad_out, T): `stats` = the natural-log LSE [2N] from forward_with_stats;
-// any other shape (e.g. the reference's [2N,2N] softmax) makes the op recompute the stats.
+// backward(z, stats, grad_out, T): the reference passes a softmax matrix here that its own
+// forward never returns (src/ntxent_kernel.cu:202). This op accepts anything in that slot and
+// recomputes the row statistics it needs (negatives-only LSE; cheap next to the backward
+// GEMMs), so results never depend on a possibly stale caller-provided softmax.
 // Returns (grad_z, grad_logits) where grad_logits = dL/dS is materialised only for 2N <= 4096.
 std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at::Tensor& stats,
                                                const at::Tensor& grad_out, double T, bool use_mixed_precision) {
+  (void)stats;
   auto z = z_in.contiguous();
-  const c10::hip::HIPGuard guard(z.device());
+  const at::DeviceGuard guard(z.device());
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
   auto pr = prep(z, *P);
   auto zqt = transpose(pr[0], *P);
-  at::Tensor lse2 = at::zeros({P->g.rows_pad}, opts(z, at::kFloat));
-  if (stats.dim() == 1 && stats.numel() == z.size(0)) {
-    lse2.narrow(0, 0, z.size(0)).copy_(stats.to(at::kFloat) * (float)1.4426950408889634);
-  } else {
-    auto fs = fwd_stats(pr[0], pr[0], *P, false);
-    lse(fs[0], pr[2], lse2, *P);
-  }
-  auto sc = coef_gemm(pr[0], pr[0], lse2, *P);
+  auto lse2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
+  auto lseneg2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
+  auto fs = fwd_stats(pr[0], pr[0], *P, false);
+  lse(fs[0], pr[2], lse2, lseneg2, *P);
+  auto sc = coef_gemm(pr[0], pr[0], lse2, pr[2], lseneg2, *P);
   auto slabs = dz(sc, zqt, *P);
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
   auto dh = norm_bwd(slabs, z, pr[1], go, *P);
