@@ -116,24 +116,24 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const Geometry& g, hipStream_t stream);
 
-// Merge the negatives-only partials -> lseneg2[i] (log2 units, local rows) and
-// lse2 = logaddexp2(lseneg2, ypos) into lse2_all[rank*Rpad + i]; loss_sum[0] receives
-// sum_i softplus(lse_neg_i - S_i,p(i)) / (W*R) over this rank's rows (all-reduce SUM across
-// ranks gives the loss). `block_loss` is scratch of Rpad/256 floats.
-void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* lseneg2,
+// Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
+// into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
+// -(sigmoid(lse_neg_i - y) + sigmoid(lse_neg_p - y)) (well conditioned when P_ip -> 1).
+// loss_sum[0] receives sum_i softplus(lse_neg_i - y_i) / (W*R) over this rank's rows
+// (all-reduce SUM across ranks gives the loss). `block_loss` is scratch of Rpad/256 floats.
+void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos,
                 float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream);
 
-// In-place: stored cosine tiles -> coefficient tiles C = P + P^T - 2 I_pos (row-major per
-// 256x256 tile; mirrors upper-triangular tiles of the own-rank block). The positive entry
-// is formed as -(sigmoid(lse_neg_i - y) + sigmoid(lse_neg_p - y)) from ypos/lseneg2, which is
-// well conditioned when P_ip -> 1.
-void launch_coef(DType comp, void* sc, const float* lse2_all, const float* ypos, const float* lseneg2,
+// Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
+// `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;
+// upper-triangular tiles of the own-rank block are mirrored; the positive entry is cpos[i].
+void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream);
 
-// Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `sc`.
-void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* sc,
-                      const float* lse2_all, const float* ypos, const float* lseneg2, const int4* tiles,
-                      int ntiles, const Geometry& g, hipStream_t stream);
+// Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `cbuf`.
+void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
+                      const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
+                      const Geometry& g, hipStream_t stream);
 
 // dZ slabs: slabs[ks][Rpad][dim_n] = C[:, K-range ks] * Z[K-range ks, :] (fp32).
 // zqt_all is [W][dim_n][Rpad] (all-gathered ZqT blocks).

@@ -12,6 +12,8 @@ namespace dev {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf168 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) void lds_void;
 

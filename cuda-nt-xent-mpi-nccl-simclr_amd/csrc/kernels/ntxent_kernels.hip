@@ -26,6 +26,9 @@ enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
 
 constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B tile = 64 KiB
 constexpr int kGemmLds = 2 * kStageBytes;             // double buffered = 128 KiB
+constexpr int kCtStride = kTile * 2 + 16;                // C^T staging row: 512 B + 16 B pad
+constexpr int kCoefLds = kTile * kCtStride;             // 132 KiB
+constexpr int kCoefWaveLds = 64 * (128 * 2 + 16);      // 17 KiB: C^T of one 128x64 wave region
 
 struct OperandDesc {
   const char* base;            // bytes
@@ -40,12 +43,13 @@ struct SimParams {
   const int4* tiles;
   long long kbytes;      // K bytes handled by one workgroup
   int R, Rpad, n_half, own0, row_tile0, col_tiles;
-  float y_scale;         // inv_temp * log2(e)
+  float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
+  int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
-  char* sc;              // tile-blocked cosine / coefficient buffer
+  char* sc;              // kept cosines: [n_fwd_tiles][256*256] (fragment order)
+  char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
   const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
-  const float* ypos;     // [R] positive logit (log2 units, from the quantised rows)
-  const float* lseneg2;  // [Rpad] log2-sum-exp2 over the NEGATIVES of each local row
+  const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
   float* out;            // dZ slabs
   long long ldo;         // elements
   long long slab_stride; // elements
@@ -58,11 +62,25 @@ struct SimParams {
 // written row-major into slot (mt, nt) and, for a mirrored tile, transposed into the
 // lower-triangular slot (nt_local, row_tile0 + mt). C is symmetric, so the mirror is exact.
 // ------------------------------------------------------------------------------------
-template <typename T>
-__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt, int kind,
+// NW = waves of the calling block: 8 (a GEMM block: the whole 256x256 tile) or 1 (a single
+// wave owning its 128x64 region; 17 KiB of LDS, so the memory-bound store-mode pass runs
+// many independent waves per CU).
+template <typename T, int NW>
+__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt, int kind, lds_char* lds,
                                               const SimParams& p, int wm, int wn, int lane) {
-  T* base = reinterpret_cast<T*>(p.sc);
+  constexpr int NROWS = NW == 8 ? kTile : 128;
+  constexpr int NCOLS = NW == 8 ? kTile : 64;
+  constexpr int S = NROWS * 2 + 16;          // LDS row stride (bytes) of the C^T staging tile
+  constexpr int NT = NW * 64;                // threads in the calling block
+  const int row_base = NW == 8 ? 0 : 128 * wm;
+  const int col_base = NW == 8 ? 0 : 64 * wn;
+  T* base = reinterpret_cast<T*>(p.cbuf);
   const int col_local0 = (nt * kTile) % p.Rpad;  // rank-local column of this tile's col 0
+  // C_ij = 2^(y - lse2_i) + 2^(y - lse2_j). Fixed-shift form (2M < 120, see the forward
+  // epilogue): 2^(y - M) * (2^(M - lse2_i) + 2^(M - lse2_j)), one exp2 per element, the
+  // per-row / per-column factors computed once.
+  const bool fixed = p.fixed_shift != 0;
+  const float M = p.y_scale;
   float lcol[4];
   bool cvalid[4];
   int gj[4];
@@ -70,7 +88,8 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt
   for (int ni = 0; ni < 4; ++ni) {
     const int col_t = 64 * wn + 16 * ni + (lane & 15);
     gj[ni] = nt * kTile + col_t;
-    lcol[ni] = p.lse2[gj[ni]];
+    const float l = p.lse2[gj[ni]];
+    lcol[ni] = fixed ? fast_exp2(M - l) : l;
     cvalid[ni] = (col_local0 + col_t) < p.R;
   }
   T* slot = base + ((long long)mt * p.col_tiles + nt) * kTileElems;
@@ -80,26 +99,21 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
     float c[4][4];
+    const int gi0 = mt * kTile + 128 * wm + 16 * mi + 4 * (lane >> 4);  // 4 consecutive rows
+    const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
+    const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row_t = 128 * wm + 16 * mi + 4 * (lane >> 4) + r;
-      const int gi = mt * kTile + row_t;
+      const int gi = gi0 + r;
       const bool rvalid = gi < p.R;
-      const float lrow = p.lse2[p.own0 + gi];
+      const float lrow = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
       const int gself = p.own0 + gi;
-      const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
-      const int gpos = p.own0 + lpos;
-      // positive: P_ip - 1 = -sigmoid(lse_neg_i - y_ip) (no 1 - P cancellation when P ~ 1)
-      float cpos = 0.f;
-      if (rvalid) {
-        const float yp = p.ypos[gi];
-        cpos = -(1.0f / (1.0f + fast_exp2(yp - p.lseneg2[gi])) + 1.0f / (1.0f + fast_exp2(yp - p.lseneg2[lpos])));
-      }
+      const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const float y = acc[mi][ni][r] * p.y_scale;
-        float v = fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
-        v = (gj[ni] == gpos) ? cpos : v;
+        float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
+        v = (gj[ni] == gpos) ? cpos4[r] : v;  // positive: -(a_i + a_p), no 1 - P cancellation
         v = (rvalid && cvalid[ni] && gj[ni] != gself) ? v : 0.0f;
         c[ni][r] = v;
       }
@@ -108,18 +122,61 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt
     for (int ni = 0; ni < 4; ++ni) {
       const int col_t = 64 * wn + 16 * ni + (lane & 15);
       const int row_t0 = 128 * wm + 16 * mi + 4 * (lane >> 4);
+      if constexpr (sizeof(T) == 2) {
+        // stage C^T in LDS: Ct[col][row0..row0+3] (one ds_write_b64 per fragment)
+        union { T h[4]; u32x2 u; } pk;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) slot[(row_t0 + r) * kTile + col_t] = from_f32<T>(c[ni][r]);
-      if (mirror) {
-        T* dst = mirror + col_t * kTile + row_t0;
-        if constexpr (sizeof(T) == 2) {
-          union { T h[4]; uint2 u; } pk;
+        for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(c[ni][r]);
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(lds + (col_t - col_base) * S + (row_t0 - row_base) * 2) = pk.u;
+      } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(c[ni][r]);
-          *reinterpret_cast<uint2*>(dst) = pk.u;
-        } else {
-          *reinterpret_cast<f32x4*>(dst) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
-        }
+        for (int r = 0; r < 4; ++r) slot[(row_t0 + r) * kTile + col_t] = c[ni][r];
+        if (mirror)
+          *reinterpret_cast<f32x4*>(mirror + col_t * kTile + row_t0) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
+      }
+    }
+  }
+  if constexpr (sizeof(T) == 2) {
+    __syncthreads();
+    const int tid = threadIdx.x, w = tid >> 6;  // w = wave index inside the calling block
+    // (a) Ct rows are rows of C^T: coalesced 16-B stores into the mirror slot (SymOff) or,
+    //     for a diagonal tile (C symmetric inside it), into the tile's own slot.
+    T* rows_dst = mirror;  // only mirrored tiles (a diagonal tile goes through (b) like any other)
+    if (rows_dst) {
+      constexpr int CPR = NROWS * 2 / 16;  // 16-B chunks per staged row
+#pragma unroll 4
+      for (int q = 0; q < NCOLS * CPR / NT; ++q) {
+        const int k = tid + NT * q;
+        const int row = k / CPR, c16 = k % CPR;
+        const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(rows_dst) + (col_base + row) * (kTile * 2) + row_base * 2 +
+                                  c16 * 16) = v;
+      }
+    }
+    // (b) rows of C = columns of Ct via the gfx950 transposed LDS read (ds_read_b64_tr_b16):
+    //     a 16-lane group reads a 4 (Ct rows) x 16 (Ct cols) block and lane i receives column
+    //     i, i.e. 4 consecutive entries of C row c0+i. Two reads give 16 B per lane.
+    {
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      constexpr int RB = NROWS / 16;                 // 16-row blocks of C in this call
+      constexpr int NBLK = RB * (NCOLS / 32) / NW;   // 16x32 blocks per wave (= 16)
+      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
+#pragma unroll 2
+      for (int b = 0; b < NBLK; ++b) {
+        const int blk = w * NBLK + b;
+        const int c0 = (blk % RB) * 16;   // C rows row_base+c0 .. +15
+        const int rb = (blk / RB) * 32;   // C cols col_base+rb .. +31
+        const int r0 = rb + 8 * g;
+        const lds_char* a0 = lds + (r0 + q4) * S + (c0 + 4 * p4) * 2;
+        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * S));
+        u32x4 u;
+        u[0] = (unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+        u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+        u[2] = (unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+        u[3] = (unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
+                                  (col_base + r0) * 2) = u;
       }
     }
   }
@@ -137,7 +194,7 @@ template <typename T, int MODE>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[kGemmLds];
+  __shared__ __attribute__((aligned(16))) char smem[MODE == kModeCoef ? kCoefLds : kGemmLds];
   lds_char* lds = (lds_char*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -233,11 +290,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       }
     }
   } else if constexpr (MODE == kModeCoef) {
-    coef_epilogue<T>(acc, mt, nt, t.z, p, wm, wn, lane);
+    coef_epilogue<T, 8>(acc, mt, nt, t.z, lds, p, wm, wn, lane);
   } else {
     const int kind = t.z;
-    if (p.sc) {  // keep cosines for the backward (fragment order; 8/16 B per lane)
-      T* st = reinterpret_cast<T*>(p.sc) + ((long long)mt * p.col_tiles + nt) * kTileElems;
+    if (p.sc) {  // keep cosines for the backward (compact: one slot per computed tile, fragment order)
+      T* st = reinterpret_cast<T*>(p.sc) + (long long)xcd_remap(blockIdx.x, gridDim.x) * kTileElems;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -265,6 +322,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       cloc[ni] = col_local0 + 64 * wn + 16 * ni + (lane & 15);
       cvalid[ni] = cloc[ni] < p.R;
     }
+    // Fixed-shift fast path: rows are unit-norm, so y = cos * M with M = log2(e)/tau and
+    // y - M lies in [-2M, 0]. For 2M < 120 every exp2(y - M) is a normal fp32 number, so ONE
+    // exp2 per element feeds both the row and the column partial with a common shift M (no
+    // max passes). Smaller tau falls back to per-tile max shifting (2 exps per element).
+    const bool fixed = p.fixed_shift != 0;
+    const float M = p.y_scale;
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -275,11 +338,36 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
-          acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
+          if (fixed)
+            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.y_scale - M) : 0.f;
+          else
+            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
         }
       }
     float2* rowred = reinterpret_cast<float2*>(smem);             // [4][256]
     float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2][256]
+    if (fixed) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
+          s = row16_sum(s);
+          if ((lane & 15) == 0)
+            rowred[wn * 256 + 128 * wm + 16 * mi + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
+        }
+      if (kind == kTileSymOff) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          float s = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+            s += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
+          s = xrow_sum(s);
+          if ((lane >> 4) == 0) colred[wm * 256 + 64 * wn + 16 * ni + lane] = make_float2(s > 0.f ? M : kNegInf, s);
+        }
+      }
+    } else {
     // row partials over this wave's 64 columns
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
@@ -312,6 +400,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         if ((lane >> 4) == 0) colred[wm * 256 + 64 * wn + 16 * ni + lane] = make_float2(m, s);
       }
     }
+    }  // !fixed
     __syncthreads();
     if (tid < 256) {
       float2 v = rowred[tid];
@@ -334,12 +423,18 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 }
 
 // Store-mode coefficient pass: read the kept cosine tile (fragment order), emit C in place.
+// Store-mode coefficient pass: one wave per 128x64 region of a kept cosine tile (fragment
+// order, 16 KiB contiguous per region) -> C into the separate coefficient buffer. 17 KiB of
+// LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound).
 template <typename T>
-__global__ __launch_bounds__(kGemmThreads) void coef_kernel(const SimParams p) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+__global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
+  const int lane = threadIdx.x;
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);
+  const int tidx = idx >> 3, w = idx & 7;
   const int wm = w >> 2, wn = w & 3;
-  const int4 t = p.tiles[xcd_remap(blockIdx.x, gridDim.x)];
-  const T* st = reinterpret_cast<const T*>(p.sc) + ((long long)t.x * p.col_tiles + t.y) * kTileElems;
+  const int4 t = p.tiles[tidx];
+  const T* st = reinterpret_cast<const T*>(p.sc) + (long long)tidx * kTileElems;
   f32x4 acc[8][4];
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
@@ -347,15 +442,14 @@ __global__ __launch_bounds__(kGemmThreads) void coef_kernel(const SimParams p) {
     for (int ni = 0; ni < 4; ++ni) {
       const T* src = st + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4;
       if constexpr (sizeof(T) == 2) {
-        union { T h[4]; uint2 u; } pk;
-        pk.u = *reinterpret_cast<const uint2*>(src);
+        union { T h[4]; u32x2 u; } pk;
+        pk.u = *reinterpret_cast<const u32x2*>(src);
         acc[mi][ni] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
       } else {
         acc[mi][ni] = *reinterpret_cast<const f32x4*>(src);
       }
     }
-  __syncthreads();  // every wave holds its cosines before the tile is overwritten in place
-  coef_epilogue<T>(acc, t.x, t.y, t.z, p, wm, wn, lane);
+  coef_epilogue<T, 1>(acc, t.x, t.y, t.z, (lds_char*)smem, p, wm, wn, lane);
 }
 
 // ------------------------------------------------------------------------------------
@@ -448,43 +542,75 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
   }
 }
 
+// 64x64 tile transpose with 16-byte global accesses on both sides (rows of Zq in, rows of
+// ZqT out); the LDS tile is padded by 16 B per row.
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
                                                         int Rpad, int dk) {
-  __shared__ T tile[64][65];
+  constexpr int V = 16 / sizeof(T);  // elements per 16 B
+  constexpr int CPR = 64 / V;        // 16-B chunks per 64-element row
+  __shared__ __attribute__((aligned(16))) T tile[64][64 + V];
   const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
-  for (int k = threadIdx.x; k < 4096; k += 256) {
-    const int r = k >> 6, c = k & 63;
-    tile[r][c] = (e0 + c < dk) ? zq[(long long)(j0 + r) * dk + e0 + c] : from_f32<T>(0.f);
+  for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
+    const int r = k / CPR, c = k % CPR;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * dk + e0 + c * V);
+    *reinterpret_cast<u32x4*>(&tile[r][c * V]) = v;
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < 4096; k += 256) {
-    const int r = k >> 6, c = k & 63;
-    zqt[(long long)(e0 + r) * Rpad + j0 + c] = tile[c][r];
+  for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
+    const int er = k / CPR, jc = k % CPR;
+    union { T h[V]; u32x4 u; } pk;
+#pragma unroll
+    for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][er];
+    *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * Rpad + j0 + jc * V) = pk.u;
   }
 }
 
-__global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ part, const float* __restrict__ ypos,
-                                                  float* __restrict__ lse2_all, float* __restrict__ lseneg2,
-                                                  float* __restrict__ block_loss, int R, int Rpad, int Tc, int own0) {
-  __shared__ float red[16];
-  const int i = blockIdx.x * 256 + threadIdx.x;
+// Row statistics of one row from its negatives-only partials: returns lse2 and writes the
+// natural-log loss term softplus(lse_neg - y_pos) and a = 1 - P_ip = sigmoid(lse_neg - y_pos).
+__device__ __forceinline__ float row_stats(const float2* __restrict__ part, int i, int Rpad, int Tc, float yp,
+                                           float& loss, float& a) {
   float m = kNegInf, s = 0.f;
   for (int t = 0; t < Tc; ++t) {
     const float2 v = part[(long long)t * Rpad + i];
     lse_merge(m, s, v.x, v.y);
   }
-  const bool ok = i < R;
-  const float yp = ok ? ypos[i] : 0.f;
   const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
-  // lse = logaddexp(lse_neg, y_pos); loss_i = softplus(lse_neg - y_pos) (natural log)
-  const float mx = fmaxf(neg2, yp);
+  const float mx = fmaxf(neg2, yp);  // lse = logaddexp(lse_neg, y_pos)
   const float l2 = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
-  lse2_all[own0 + i] = ok ? l2 : 0.f;
-  lseneg2[i] = ok ? neg2 : 0.f;
   const float x = (neg2 - yp) * kLn2;
-  const float sp = x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
-  const float li = ok ? sp : 0.f;
+  loss = x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
+  a = 1.0f / (1.0f + exp2f(yp - neg2));
+  return l2;
+}
+
+// One thread per positive pair (i, i+n) (plus the pad rows): LSE of both rows, their loss
+// terms, and the positive coefficient C_ip = P_ip + P_pi - 2 = -(a_i + a_p), formed without
+// the 1 - P cancellation.
+__global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ part, const float* __restrict__ ypos,
+                                                  float* __restrict__ lse2_all, float* __restrict__ cpos,
+                                                  float* __restrict__ block_loss, int R, int Rpad, int Tc, int own0) {
+  __shared__ float red[16];
+  const int n = R >> 1;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  float li = 0.f;
+  if (t < n) {
+    const int i = t, j = t + n;
+    const float yp = ypos[i];
+    float l_i, l_j, a_i, a_j;
+    const float l2i = row_stats(part, i, Rpad, Tc, yp, l_i, a_i);
+    const float l2j = row_stats(part, j, Rpad, Tc, yp, l_j, a_j);
+    lse2_all[own0 + i] = l2i;
+    lse2_all[own0 + j] = l2j;
+    cpos[i] = -(a_i + a_j);
+    cpos[j] = -(a_i + a_j);
+    li = l_i + l_j;
+  } else if (t < Rpad - n) {
+    const int i = R + (t - n);
+    lse2_all[own0 + i] = 0.f;
+    cpos[i] = 0.f;
+  }
   const float tot = block_sum(li, red);
   if (threadIdx.x == 0) block_loss[blockIdx.x] = tot;
 }
@@ -494,6 +620,53 @@ __global__ void loss_final_kernel(const float* __restrict__ block_loss, int nb, 
     float s = 0.f;
     for (int b = 0; b < nb; ++b) s += block_loss[b];  // fixed order: deterministic
     out[0] = s * scale;
+  }
+}
+
+// Vectorised normalisation backward: one 256-thread block per row; each thread owns NCH
+// chunks of 8 contiguous features, kept in registers between the dot pass and the output.
+template <typename Tin, int NCH>
+__global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int ksplit,
+                                                           long long slab_stride, long long ldo,
+                                                           const Tin* __restrict__ h, const float* __restrict__ inv,
+                                                           const float* __restrict__ grad_out, float alpha_base,
+                                                           Tin* __restrict__ dh, int d) {
+  __shared__ float red[16];
+  const int i = blockIdx.x;
+  const float iv = inv[i];
+  const float alpha = grad_out[0] * alpha_base;
+  const Tin* hi = h + (long long)i * d;
+  const float* gi = slabs + (long long)i * ldo;
+  float g[NCH][8], z[NCH][8];
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 256 + threadIdx.x) * 8;
+    if (e < d) {
+      load8<Tin>(hi + e, z[c]);
+      f32x4 a = *reinterpret_cast<const f32x4*>(gi + e), b = *reinterpret_cast<const f32x4*>(gi + e + 4);
+      for (int k = 1; k < ksplit; ++k) {
+        a += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e);
+        b += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e + 4);
+      }
+      g[c][0] = a[0]; g[c][1] = a[1]; g[c][2] = a[2]; g[c][3] = a[3];
+      g[c][4] = b[0]; g[c][5] = b[1]; g[c][6] = b[2]; g[c][7] = b[3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { z[c][j] *= iv; dot += z[c][j] * g[c][j]; }
+    }
+  }
+  dot = block_sum(dot, red);
+  Tin* di = dh + (long long)i * d;
+  const float s = alpha * iv;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 256 + threadIdx.x) * 8;
+    if (e < d) {
+      float o[8], q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = s * (g[c][j] - z[c][j] * dot);
+      store8<Tin>(di + e, o, q);
+    }
   }
 }
 
@@ -551,6 +724,7 @@ dev::SimParams base_params(const Geometry& g) {
   p.row_tile0 = g.rank * g.row_tiles;
   p.col_tiles = g.col_tiles;
   p.y_scale = g.inv_temp * dev::kLog2e;
+  p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
   return p;
 }
 
@@ -670,9 +844,9 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* sc,
-                      const float* lse2_all, const float* ypos, const float* lseneg2, const int4* tiles,
-                      int ntiles, const Geometry& g, hipStream_t stream) {
+void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
+                      const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
+                      const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   const long long kb = (long long)g.dim_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
@@ -680,10 +854,9 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   p.B = rowmajor_operand(zq_all, kb, kb);
   p.tiles = tiles;
   p.kbytes = kb;
-  p.sc = static_cast<char*>(sc);
+  p.cbuf = static_cast<char*>(cbuf);
   p.lse2 = lse2_all;
-  p.ypos = ypos;
-  p.lseneg2 = lseneg2;
+  p.cpos = cpos;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeCoef>), dim3(ntiles), dim3(kGemmThreads), 0,
@@ -692,10 +865,10 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* lseneg2, float* block_loss,
+void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
                 float* loss_sum, const Geometry& g, hipStream_t stream) {
-  const int nb = g.rows_pad / 256;
-  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, lseneg2, block_loss,
+  const int nb = (g.rows_pad - g.rows / 2 + 255) / 256;  // one thread per pair + pad rows
+  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, cpos, block_loss,
                      g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad);
   NTXENT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(dev::loss_final_kernel, dim3(1), dim3(64), 0, stream, block_loss, nb,
@@ -703,18 +876,18 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* l
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_coef(DType comp, void* sc, const float* lse2_all, const float* ypos, const float* lseneg2,
+void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
   p.tiles = tiles;
-  p.sc = static_cast<char*>(sc);
+  p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
+  p.cbuf = static_cast<char*>(cbuf);
   p.lse2 = lse2_all;
-  p.ypos = ypos;
-  p.lseneg2 = lseneg2;
+  p.cpos = cpos;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(ntiles), dim3(kGemmThreads), 0, stream, p);
+    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(8 * ntiles), dim3(64), 0, stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }
@@ -754,11 +927,25 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
 void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h, const float* inv,
                      const float* grad_out, void* dh, const Geometry& g, hipStream_t stream) {
   const float alpha_base = (float)(1.0 / ((double)g.global_rows * g.temperature));
+  const long long ss = (long long)g.rows_pad * g.dim_n, ldo = g.dim_n;
+  const int nch = (g.dim + 2047) / 2048;  // 8-element chunks per thread
+  const bool vec = (g.dim % 8) == 0 && nch <= 4;
   dispatch_comp(in, [&](auto tin) {
     using Tin = decltype(tin);
-    hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit,
-                       (long long)g.rows_pad * g.dim_n, (long long)g.dim_n, static_cast<const Tin*>(h), inv,
-                       grad_out, alpha_base, static_cast<Tin*>(dh), g.dim);
+    const Tin* hp = static_cast<const Tin*>(h);
+    Tin* dp = static_cast<Tin*>(dh);
+    if (vec && nch == 1)
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+    else if (vec && nch == 2)
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+    else if (vec)
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+    else
+      hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss, ldo,
+                         hp, inv, grad_out, alpha_base, dp, g.dim);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

@@ -146,8 +146,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos)
-    sc = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, zq_local.options());
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
@@ -155,41 +154,43 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   return {part, sc};
 }
 
-// Writes this rank's slice of lse2_all (log2 units) and lseneg2 (negatives-only LSE of the
-// local rows); returns the local loss contribution.
-at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, at::Tensor& lseneg2,
+// Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
+// -(a_i + a_p) of the local rows); returns the local loss contribution.
+at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, at::Tensor& cpos,
                const Plan& P) {
   check_input(part, "part");
   NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad && lse2_all.scalar_type() == at::kFloat,
                "lse2_all must be float32 [world*rows_pad]");
-  NTXENT_CHECK(lseneg2.numel() == P.g.rows_pad && lseneg2.scalar_type() == at::kFloat,
-               "lseneg2 must be float32 [rows_pad]");
+  NTXENT_CHECK(cpos.numel() == P.g.rows_pad && cpos.scalar_type() == at::kFloat, "cpos must be float32 [rows_pad]");
   const at::DeviceGuard guard(part.device());
   auto block_loss = at::empty({P.g.rows_pad / 256}, opts(part, at::kFloat));
   auto loss = at::empty({}, opts(part, at::kFloat));
   launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(),
-             lse2_all.data_ptr<float>(), lseneg2.data_ptr<float>(), block_loss.data_ptr<float>(),
+             lse2_all.data_ptr<float>(), cpos.data_ptr<float>(), block_loss.data_ptr<float>(),
              loss.data_ptr<float>(), P.g, cur_stream(part));
   return loss;
 }
 
-void coef(at::Tensor& sc, const at::Tensor& lse2_all, const at::Tensor& ypos, const at::Tensor& lseneg2,
-          const Plan& P) {
-  check_input(sc, "sc");
-  const at::DeviceGuard guard(sc.device());
-  launch_coef(P.comp, sc.data_ptr(), lse2_all.data_ptr<float>(), ypos.data_ptr<float>(), lseneg2.data_ptr<float>(),
-              reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sc));
+// Kept cosines (compact, one slot per forward tile) -> coefficient buffer (all tiles).
+at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P) {
+  check_input(sbuf, "sbuf");
+  NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
+  const at::DeviceGuard guard(sbuf.device());
+  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
+  launch_coef(P.comp, sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
+              reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf));
+  return cbuf;
 }
 
 at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& lse2_all,
-                     const at::Tensor& ypos, const at::Tensor& lseneg2, const Plan& P) {
+                     const at::Tensor& cpos, const Plan& P) {
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
-  auto sc = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
-  launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), sc.data_ptr(), lse2_all.data_ptr<float>(),
-                   ypos.data_ptr<float>(), lseneg2.data_ptr<float>(),
-                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(zq_local));
-  return sc;
+  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
+                   cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
+                   P.g, cur_stream(zq_local));
+  return cbuf;
 }
 
 at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
@@ -215,7 +216,7 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
 }
 
 // ---- single-process fused flows ------------------------------------------------------
-// Returns {loss, zq, zqt, inv, lse2, sc, ypos, lseneg2}; `sc` holds cosines (keep_cos) or is
+// Returns {loss, zq, zqt, inv, lse2, sc, cpos}; `sc` holds the kept cosines (keep_cos) or is
 // undefined.
 std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::string& compute, bool keep_cos) {
   check_input(h, "h");
@@ -227,25 +228,24 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   auto zqt = transpose(pr[0], *P);
   auto fs = fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-  auto lseneg2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-  auto loss = lse(fs[0], pr[2], lse2, lseneg2, *P);
-  return {loss, pr[0], zqt, pr[1], lse2, fs[1], pr[2], lseneg2};
+  auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
+  return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
 at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const at::Tensor& zqt, const at::Tensor& inv,
-                          const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& ypos,
-                          const at::Tensor& lseneg2, const at::Tensor& grad_out, double T) {
+                          const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& cpos,
+                          const at::Tensor& grad_out, double T) {
   const at::DeviceGuard guard(h.device());
   const DType comp = to_dtype(zq.scalar_type());
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
-  at::Tensor sc;
+  at::Tensor cb;
   if (sc_in.has_value() && sc_in->defined()) {
-    sc = *sc_in;
-    coef(sc, lse2, ypos, lseneg2, *P);
+    cb = coef(*sc_in, lse2, cpos, *P);
   } else {
-    sc = coef_gemm(zq, zq, lse2, ypos, lseneg2, *P);
+    cb = coef_gemm(zq, zq, lse2, cpos, *P);
   }
-  auto slabs = dz(sc, zqt, *P);
+  auto slabs = dz(cb, zqt, *P);
   return norm_bwd(slabs, h, inv, grad_out, *P);
 }
 
@@ -277,10 +277,10 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   auto pr = prep(z, *P);
   auto zqt = transpose(pr[0], *P);
   auto lse2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
-  auto lseneg2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
+  auto cpos = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
   auto fs = fwd_stats(pr[0], pr[0], *P, false);
-  lse(fs[0], pr[2], lse2, lseneg2, *P);
-  auto sc = coef_gemm(pr[0], pr[0], lse2, pr[2], lseneg2, *P);
+  lse(fs[0], pr[2], lse2, cpos, *P);
+  auto sc = coef_gemm(pr[0], pr[0], lse2, cpos, *P);
   auto slabs = dz(sc, zqt, *P);
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
   auto dh = norm_bwd(slabs, z, pr[1], go, *P);

@@ -50,20 +50,19 @@ class NTXentFunction(torch.autograd.Function):
     def forward(ctx, h: torch.Tensor, temperature: float, compute: str, keep_logits: bool):
         C = _ext.load()
         h = h.contiguous()
-        loss, zq, zqt, inv, lse2, sc, ypos, lseneg2 = C.fused_forward(h, float(temperature), compute,
-                                                                       bool(keep_logits))
+        loss, zq, zqt, inv, lse2, sc, cpos = C.fused_forward(h, float(temperature), compute, bool(keep_logits))
         ctx.temperature = float(temperature)
-        ctx.sc = sc if keep_logits else None  # consumed (overwritten) by the first backward
-        ctx.save_for_backward(h, zq, zqt, inv, lse2, ypos, lseneg2)
+        ctx.sc = sc if keep_logits else None  # released by the first backward
+        ctx.save_for_backward(h, zq, zqt, inv, lse2, cpos)
         ctx.mark_non_differentiable()
         return loss
 
     @staticmethod
     def backward(ctx, grad_out: torch.Tensor):
         C = _ext.load()
-        h, zq, zqt, inv, lse2, ypos, lseneg2 = ctx.saved_tensors
+        h, zq, zqt, inv, lse2, cpos = ctx.saved_tensors
         sc, ctx.sc = ctx.sc, None  # a second backward (retain_graph) recomputes the cosines
-        dh = C.fused_backward(h, zq, zqt, inv, lse2, sc, ypos, lseneg2, grad_out.reshape(1), ctx.temperature)
+        dh = C.fused_backward(h, zq, zqt, inv, lse2, sc, cpos, grad_out.reshape(1), ctx.temperature)
         return dh, None, None, None
 
 

@@ -56,8 +56,8 @@ class DistNTXentFunction(torch.autograd.Function):
             zq_all, zqt_all, work_t = zq, zqt.unsqueeze(0), None
         part, sc = C.fwd_stats(zq, zq_all, plan, bool(keep_logits))
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
-        lseneg2 = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
-        loss = C.lse(part, ypos, lse2_all, lseneg2, plan)
+        cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
+        loss = C.lse(part, ypos, lse2_all, cpos, plan)
         if W > 1:
             mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
             dist.all_gather_into_tensor(lse2_all, mine, group=group)
@@ -65,21 +65,21 @@ class DistNTXentFunction(torch.autograd.Function):
         ctx.plan = plan
         ctx.work_t = work_t
         ctx.sc = sc if keep_logits else None
-        ctx.save_for_backward(h, zq, zq_all, zqt_all, inv, lse2_all, ypos, lseneg2)
+        ctx.save_for_backward(h, zq, zq_all, zqt_all, inv, lse2_all, cpos)
         return loss
 
     @staticmethod
     def backward(ctx, grad_out: torch.Tensor):
         C = _ext.load()
-        h, zq, zq_all, zqt_all, inv, lse2_all, ypos, lseneg2 = ctx.saved_tensors
+        h, zq, zq_all, zqt_all, inv, lse2_all, cpos = ctx.saved_tensors
         if ctx.work_t is not None:
             ctx.work_t.wait()
             ctx.work_t = None
         sc, ctx.sc = ctx.sc, None
         if sc is not None:
-            C.coef(sc, lse2_all, ypos, lseneg2, ctx.plan)
+            sc = C.coef(sc, lse2_all, cpos, ctx.plan)
         else:
-            sc = C.coef_gemm(zq, zq_all, lse2_all, ypos, lseneg2, ctx.plan)
+            sc = C.coef_gemm(zq, zq_all, lse2_all, cpos, ctx.plan)
         slabs = C.dz(sc, zqt_all, ctx.plan)
         dh = C.norm_bwd(slabs, h, inv, grad_out.reshape(1), ctx.plan)
         return dh, None, None, None, None, None

@@ -119,16 +119,16 @@ def build_cpp_targets(k_obj: Path, force: bool = False, verbose: bool = False):
         "ntxent_bench": ROOT / "bench" / "ntxent_bench.cpp",
         "ntxent_tests": ROOT / "tests" / "cpp" / "ntxent_tests.cpp",
     }
-    jobs = []
-    for name, src in targets.items():
-        if not src.exists():
-            continue
+    def one(name, src):
         out = BUILD / "bin" / name
+        obj = BUILD / f"{name}.o"
         if force or _stale(out, [src, k_obj, *hdrs]):
-            jobs.append([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O2", f"-I{CSRC / 'include'}",
-                         str(src), str(k_obj), "-o", str(out)])
+            _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O2", f"-I{CSRC / 'include'}", "-c", str(src),
+                  "-o", str(obj)], verbose)
+            _run([HIPCC, f"--offload-arch={ARCH}", str(obj), str(k_obj), "-o", str(out)], verbose)
+
     with cf.ThreadPoolExecutor(max_workers=2) as ex:
-        list(ex.map(lambda c: _run(c, verbose), jobs))
+        list(ex.map(lambda kv: one(*kv), [(n, s) for n, s in targets.items() if s.exists()]))
 
 
 def main():
