@@ -90,8 +90,8 @@ class Bench {
     b_.n_dz = (int)dt.size();
     NTXENT_HIP_CHECK(hipMalloc(&b_.h, R * dim * is));
     NTXENT_HIP_CHECK(hipMalloc(&b_.dh, R * dim * is));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.zq, Rp * g_.dim_k * cs));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.zqt, (size_t)g_.dim_n * Rp * cs));
+    NTXENT_HIP_CHECK(hipMalloc(&b_.zq, Rp * g_.ld_k * cs));
+    NTXENT_HIP_CHECK(hipMalloc(&b_.zqt, (size_t)g_.dim_n * g_.ld_t * cs));
     NTXENT_HIP_CHECK(hipMalloc(&b_.inv, R * 4));
     NTXENT_HIP_CHECK(hipMalloc(&b_.ypos, R * 4));
     NTXENT_HIP_CHECK(hipMalloc(&b_.part, (size_t)g_.col_tiles * Rp * 8));
@@ -139,24 +139,27 @@ class Bench {
       NTXENT_HIP_CHECK(hipMemcpy(b_.h, h16.data(), R * dim * 2, hipMemcpyHostToDevice));
     }
     NTXENT_HIP_CHECK(hipStreamCreate(&s_));
+    ws_.num_cus = ncus;
+    ws_.bytes = gemm_workspace_bytes(std::max(b_.n_fwd, b_.n_dz), ncus);
+    NTXENT_HIP_CHECK(hipMalloc(&ws_.ptr, ws_.bytes));
   }
   ~Bench() {
     hipFree(b_.h); hipFree(b_.dh); hipFree(b_.zq); hipFree(b_.zqt); hipFree(b_.inv); hipFree(b_.ypos);
     hipFree(b_.part); hipFree(b_.sbuf); hipFree(b_.cbuf); hipFree(b_.lse2); hipFree(b_.cpos);
     hipFree(b_.block_loss); hipFree(b_.loss); hipFree(b_.grad_out); hipFree(b_.slabs);
-    hipFree(b_.fwd_tiles); hipFree(b_.dz_tiles);
+    hipFree(b_.fwd_tiles); hipFree(b_.dz_tiles); hipFree(ws_.ptr);
     hipStreamDestroy(s_);
   }
 
   void fwd() {
     launch_prep(in_, comp_, b_.h, b_.zq, b_.inv, b_.ypos, g_, s_);
     launch_transpose(comp_, b_.zq, b_.zqt, g_, s_);
-    launch_fwd_stats(comp_, b_.zq, b_.zq, b_.fwd_tiles, b_.n_fwd, b_.part, b_.sbuf, g_, s_);
+    launch_fwd_stats(comp_, b_.zq, b_.zq, b_.fwd_tiles, b_.n_fwd, b_.part, b_.sbuf, ws_, g_, s_);
     launch_lse(b_.part, b_.ypos, b_.lse2, b_.cpos, b_.block_loss, b_.loss, g_, s_);
   }
   void bwd() {
     launch_coef(comp_, b_.sbuf, b_.cbuf, b_.lse2, b_.cpos, b_.fwd_tiles, b_.n_fwd, g_, s_);
-    launch_dz(comp_, b_.cbuf, b_.zqt, b_.dz_tiles, b_.n_dz, b_.ksplit, b_.slabs, g_, s_);
+    launch_dz(comp_, b_.cbuf, b_.zqt, b_.dz_tiles, b_.n_dz, b_.slabs, ws_, g_, s_);
     launch_norm_bwd(in_, b_.slabs, b_.ksplit, b_.h, b_.inv, b_.grad_out, b_.dh, g_, s_);
   }
 
@@ -230,6 +233,7 @@ class Bench {
   DType in_, comp_;
   Geometry g_;
   Buffers b_;
+  GemmWorkspace ws_;
   hipStream_t s_ = nullptr;
   std::vector<float> host_;
 };

@@ -20,8 +20,10 @@
 // Layout conventions (see Geometry):
 //   * R local rows = [view1 (n rows); view2 (n rows)], positive p(i) = (i + n) mod R.
 //   * Global column index = rank * Rpad + local row (padded rank blocks).
-//   * Zq   [Rpad][dim_k]     normalised rows in the compute dtype (zero padded).
-//   * ZqT  [dim_n][Rpad]     its transpose (B operand of the dZ GEMM).
+//   * Zq   [Rpad][ld_k]      normalised rows in the compute dtype (zero padded to dim_k).
+//   * ZqT  [dim_n][ld_t]     its transpose (B operand of the dZ GEMM), columns [0, Rpad).
+//     ld_k / ld_t add 128 B to strides that are multiples of 2 KiB, so the 256 rows a GEMM
+//     tile streams do not all land in the same L2 channel.
 //   * SC   [row_tiles][col_tiles][256*256]  tile-blocked cosines / coefficients.
 #pragma once
 
@@ -75,6 +77,8 @@ struct Geometry {
   int dim = 0;         // d
   int dim_k = 0;       // roundup(d, 64): row stride of Zq (K of the forward GEMM)
   int dim_n = 0;       // roundup(d, 256): rows of ZqT (N of the dZ GEMM)
+  int ld_k = 0;        // row stride (elements) of Zq: dim_k, de-aliased from powers of two
+  int ld_t = 0;        // row stride (elements) of ZqT: rows_pad, de-aliased likewise
   int world = 1;       // W ranks sharing negatives
   int rank = 0;
   int row_tiles = 0;   // Rpad / 256
@@ -93,8 +97,27 @@ enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2 };
 std::vector<int4> build_fwd_tiles(const Geometry& g);
 // dZ tiles (ti, tn, ks, 0) for a split-K factor.
 std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit);
-// Split-K factor that fills `num_cus` compute units with dZ tiles.
+// Split-K factor for the dZ GEMM; the stream-K schedule balances K itself, so this is 1.
 int choose_dz_ksplit(const Geometry& g, int num_cus);
+
+// Persistent stream-K schedule of the similarity GEMMs: `grid` blocks first process
+// `dp_tiles` whole tiles in rounds, then split the K-steps of the remaining `sk_tiles` tiles
+// evenly (`ipb` steps per block); a split tile is reduced and finished deterministically by
+// its last-arriving block. This removes the tile-count quantisation of a plain one-block-per-
+// tile launch (e.g. 528 forward tiles on 256 CUs would need 3 rounds instead of 2.06).
+struct GemmSchedule {
+  int grid = 0, nk = 0, dp_tiles = 0, sk_tiles = 0;
+  long long ipb = 0;
+};
+GemmSchedule make_schedule(int ntiles, int nk, int num_cus);
+
+// Scratch of one similarity-GEMM launch: arrival counters + 2 fp32 partial tiles per block.
+struct GemmWorkspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int num_cus = 256;
+};
+size_t gemm_workspace_bytes(int ntiles, int num_cus);
 
 // ---- device-side launchers (all asynchronous on `stream`, no host syncs, no mallocs:
 //      safe under hipGraph capture) -----------------------------------------------------
@@ -114,7 +137,7 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g,
 // cosine tile is kept (compute dtype, fragment order) for the backward.
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
-                      const Geometry& g, hipStream_t stream);
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
 
 // Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
@@ -133,12 +156,12 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 // Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `cbuf`.
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
-                      const Geometry& g, hipStream_t stream);
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
 
-// dZ slabs: slabs[ks][Rpad][dim_n] = C[:, K-range ks] * Z[K-range ks, :] (fp32).
-// zqt_all is [W][dim_n][Rpad] (all-gathered ZqT blocks).
-void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles,
-               int ntiles, int ksplit, float* slabs, const Geometry& g, hipStream_t stream);
+// dZ[Rpad][dim_n] = C * Z (fp32), C = the coefficient buffer, zqt_all = [W][dim_n][Rpad]
+// (all-gathered ZqT blocks); tiles from build_dz_tiles(g, 1).
+void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
+               float* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
 
 // dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
 void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,

@@ -14,443 +14,15 @@
 
 #include "../include/ntxent/ntxent.h"
 #include "device_common.h"
+#include "sim_gemm.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
 namespace ntxent {
 namespace dev {
-
-enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
-
-constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B tile = 64 KiB
-constexpr int kGemmLds = 2 * kStageBytes;             // double buffered = 128 KiB
-constexpr int kCtStride = kTile * 2 + 16;                // C^T staging row: 512 B + 16 B pad
-constexpr int kCoefLds = kTile * kCtStride;             // 132 KiB
-constexpr int kCoefWaveLds = 64 * (128 * 2 + 16);      // 17 KiB: C^T of one 128x64 wave region
-
-struct OperandDesc {
-  const char* base;            // bytes
-  long long row_tile_stride;   // bytes between consecutive 256-row tiles
-  long long ld;                // bytes between rows inside a tile
-  long long kblk;              // K bytes per contiguous K block
-  long long kblk_stride;       // bytes between K blocks
-};
-
-struct SimParams {
-  OperandDesc A, B;
-  const int4* tiles;
-  long long kbytes;      // K bytes handled by one workgroup
-  int R, Rpad, n_half, own0, row_tile0, col_tiles;
-  float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
-  int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
-  float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
-  char* sc;              // kept cosines: [n_fwd_tiles][256*256] (fragment order)
-  char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
-  const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
-  const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
-  float* out;            // dZ slabs
-  long long ldo;         // elements
-  long long slab_stride; // elements
-};
-
-// ------------------------------------------------------------------------------------
-// Coefficient epilogue shared by the store-mode coef kernel and the recompute GEMM:
-// cos tile (MFMA C layout, rows = local rows of tile mt, cols = global cols of tile nt)
-//   -> C_ij = 2^(y - lse2_i) + 2^(y - lse2_j) - 2[j == p(i)],  0 on the diagonal / padding
-// written row-major into slot (mt, nt) and, for a mirrored tile, transposed into the
-// lower-triangular slot (nt_local, row_tile0 + mt). C is symmetric, so the mirror is exact.
-// ------------------------------------------------------------------------------------
-// NW = waves of the calling block: 8 (a GEMM block: the whole 256x256 tile) or 1 (a single
-// wave owning its 128x64 region; 17 KiB of LDS, so the memory-bound store-mode pass runs
-// many independent waves per CU).
-template <typename T, int NW>
-__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], int mt, int nt, int kind, lds_char* lds,
-                                              const SimParams& p, int wm, int wn, int lane) {
-  constexpr int NROWS = NW == 8 ? kTile : 128;
-  constexpr int NCOLS = NW == 8 ? kTile : 64;
-  constexpr int S = NROWS * 2 + 16;          // LDS row stride (bytes) of the C^T staging tile
-  constexpr int NT = NW * 64;                // threads in the calling block
-  const int row_base = NW == 8 ? 0 : 128 * wm;
-  const int col_base = NW == 8 ? 0 : 64 * wn;
-  T* base = reinterpret_cast<T*>(p.cbuf);
-  const int col_local0 = (nt * kTile) % p.Rpad;  // rank-local column of this tile's col 0
-  // C_ij = 2^(y - lse2_i) + 2^(y - lse2_j). Fixed-shift form (2M < 120, see the forward
-  // epilogue): 2^(y - M) * (2^(M - lse2_i) + 2^(M - lse2_j)), one exp2 per element, the
-  // per-row / per-column factors computed once.
-  const bool fixed = p.fixed_shift != 0;
-  const float M = p.y_scale;
-  float lcol[4];
-  bool cvalid[4];
-  int gj[4];
-#pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int col_t = 64 * wn + 16 * ni + (lane & 15);
-    gj[ni] = nt * kTile + col_t;
-    const float l = p.lse2[gj[ni]];
-    lcol[ni] = fixed ? fast_exp2(M - l) : l;
-    cvalid[ni] = (col_local0 + col_t) < p.R;
-  }
-  T* slot = base + ((long long)mt * p.col_tiles + nt) * kTileElems;
-  T* mirror = nullptr;
-  if (kind == kTileSymOff)
-    mirror = base + ((long long)(nt - p.row_tile0) * p.col_tiles + p.row_tile0 + mt) * kTileElems;
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    float c[4][4];
-    const int gi0 = mt * kTile + 128 * wm + 16 * mi + 4 * (lane >> 4);  // 4 consecutive rows
-    const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
-    const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int gi = gi0 + r;
-      const bool rvalid = gi < p.R;
-      const float lrow = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
-      const int gself = p.own0 + gi;
-      const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const float y = acc[mi][ni][r] * p.y_scale;
-        float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
-        v = (gj[ni] == gpos) ? cpos4[r] : v;  // positive: -(a_i + a_p), no 1 - P cancellation
-        v = (rvalid && cvalid[ni] && gj[ni] != gself) ? v : 0.0f;
-        c[ni][r] = v;
-      }
-    }
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int col_t = 64 * wn + 16 * ni + (lane & 15);
-      const int row_t0 = 128 * wm + 16 * mi + 4 * (lane >> 4);
-      if constexpr (sizeof(T) == 2) {
-        // stage C^T in LDS: Ct[col][row0..row0+3] (one ds_write_b64 per fragment)
-        union { T h[4]; u32x2 u; } pk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(c[ni][r]);
-        *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(lds + (col_t - col_base) * S + (row_t0 - row_base) * 2) = pk.u;
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) slot[(row_t0 + r) * kTile + col_t] = c[ni][r];
-        if (mirror)
-          *reinterpret_cast<f32x4*>(mirror + col_t * kTile + row_t0) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
-      }
-    }
-  }
-  if constexpr (sizeof(T) == 2) {
-    __syncthreads();
-    const int tid = threadIdx.x, w = tid >> 6;  // w = wave index inside the calling block
-    // (a) Ct rows are rows of C^T: coalesced 16-B stores into the mirror slot (SymOff) or,
-    //     for a diagonal tile (C symmetric inside it), into the tile's own slot.
-    T* rows_dst = mirror;  // only mirrored tiles (a diagonal tile goes through (b) like any other)
-    if (rows_dst) {
-      constexpr int CPR = NROWS * 2 / 16;  // 16-B chunks per staged row
-#pragma unroll 4
-      for (int q = 0; q < NCOLS * CPR / NT; ++q) {
-        const int k = tid + NT * q;
-        const int row = k / CPR, c16 = k % CPR;
-        const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(rows_dst) + (col_base + row) * (kTile * 2) + row_base * 2 +
-                                  c16 * 16) = v;
-      }
-    }
-    // (b) rows of C = columns of Ct via the gfx950 transposed LDS read (ds_read_b64_tr_b16):
-    //     a 16-lane group reads a 4 (Ct rows) x 16 (Ct cols) block and lane i receives column
-    //     i, i.e. 4 consecutive entries of C row c0+i. Two reads give 16 B per lane.
-    {
-      typedef short v4s __attribute__((ext_vector_type(4)));
-      constexpr int RB = NROWS / 16;                 // 16-row blocks of C in this call
-      constexpr int NBLK = RB * (NCOLS / 32) / NW;   // 16x32 blocks per wave (= 16)
-      const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
-#pragma unroll 2
-      for (int b = 0; b < NBLK; ++b) {
-        const int blk = w * NBLK + b;
-        const int c0 = (blk % RB) * 16;   // C rows row_base+c0 .. +15
-        const int rb = (blk / RB) * 32;   // C cols col_base+rb .. +31
-        const int r0 = rb + 8 * g;
-        const lds_char* a0 = lds + (r0 + q4) * S + (c0 + 4 * p4) * 2;
-        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
-        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * S));
-        u32x4 u;
-        u[0] = (unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
-        u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
-        u[2] = (unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
-        u[3] = (unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
-                                  (col_base + r0) * 2) = u;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// The similarity GEMM: out tile (256x256) = A_tile (256 x K) * B_tile (256 x K)^T, both
-// operands K-contiguous. 8 waves (2 M x 4 N), 128x64 outputs per wave as 8x4 MFMA 16x16
-// accumulators. K advances 128 bytes per step through a 2-deep LDS ring filled by
-// global_load_lds_dwordx4 (lane-linear destination, swizzle applied on the source side:
-// physical 16B chunk = logical ^ ((row>>1)&7), conflict-free for the ds_read_b128 lane
-// groups of the 16x16x32 operand reads).
-// ------------------------------------------------------------------------------------
-template <typename T, int MODE>
-__global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
-  typedef typename Mfma<T>::frag frag;
-  typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[MODE == kModeCoef ? kCoefLds : kGemmLds];
-  lds_char* lds = (lds_char*)smem;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 2, wn = w & 3;
-  const int4 t = p.tiles[xcd_remap(blockIdx.x, gridDim.x)];
-  const int mt = t.x, nt = t.y;
-
-  const char* Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
-  const char* Bb = p.B.base + (long long)nt * p.B.row_tile_stride;
-  long long k0 = (MODE == kModeDz) ? (long long)t.z * p.kbytes : 0;
-  long long a_kin = k0 % p.A.kblk, a_kbo = (k0 / p.A.kblk) * p.A.kblk_stride;
-  long long b_kin = k0 % p.B.kblk, b_kbo = (k0 / p.B.kblk) * p.B.kblk_stride;
-
-  // per-lane staging offsets (constant over K)
-  unsigned a_off[4], b_off[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = (4 * w + q) * 8 + (lane >> 3);
-    const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
-    a_off[q] = (unsigned)(row * p.A.ld) + lchunk * 16;
-    b_off[q] = (unsigned)(row * p.B.ld) + lchunk * 16;
-  }
-
-  auto stage = [&](int buf) {
-    lds_char* As = lds + buf * kStageBytes;
-    lds_char* Bs = As + kTile * kKStepBytes;
-    const char* ak = Ab + a_kbo + a_kin;
-    const char* bk = Bb + b_kbo + b_kin;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int g = 4 * w + q;
-      __builtin_amdgcn_global_load_lds((const void*)(ak + a_off[q]), (lds_void*)(As + g * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(bk + b_off[q]), (lds_void*)(Bs + g * 1024),
-                                       16, 0, 0);
-    }
-    a_kin += kKStepBytes;
-    if (a_kin == p.A.kblk) { a_kin = 0; a_kbo += p.A.kblk_stride; }
-    b_kin += kKStepBytes;
-    if (b_kin == p.B.kblk) { b_kin = 0; b_kbo += p.B.kblk_stride; }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
-  auto compute = [&](int buf) {
-    const lds_char* As = lds + buf * kStageBytes;
-    const lds_char* Bs = As + kTile * kKStepBytes;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int pch = ((4 * s + cq) ^ sw) << 4;
-      frag a[8], b[4];
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-        a[mi] = *(lds_frag*)(As + (128 * wm + 16 * mi + r16) * kKStepBytes + pch);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        b[ni] = *(lds_frag*)(Bs + (64 * wn + 16 * ni + r16) * kKStepBytes + pch);
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          acc[mi][ni] = (MODE == kModeDz) ? Mfma<T>::mma(b[ni], a[mi], acc[mi][ni])
-                                          : Mfma<T>::mma(a[mi], b[ni], acc[mi][ni]);
-    }
-  };
-
-  const int nk = (int)(p.kbytes / kKStepBytes);
-  stage(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int it = 0; it < nk; ++it) {
-    if (it + 1 < nk) stage((it + 1) & 1);
-    compute(it & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-  if constexpr (MODE == kModeDz) {
-    // swapped orientation: lane holds out[m = 16mi + (lane&15)][n = 16ni + 4(lane>>4) + r]
-    float* out = p.out + (long long)t.z * p.slab_stride;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const long long row = (long long)mt * kTile + 128 * wm + 16 * mi + (lane & 15);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int col = nt * kTile + 64 * wn + 16 * ni + 4 * (lane >> 4);
-        *reinterpret_cast<f32x4*>(out + row * p.ldo + col) = acc[mi][ni];
-      }
-    }
-  } else if constexpr (MODE == kModeCoef) {
-    coef_epilogue<T, 8>(acc, mt, nt, t.z, lds, p, wm, wn, lane);
-  } else {
-    const int kind = t.z;
-    if (p.sc) {  // keep cosines for the backward (compact: one slot per computed tile, fragment order)
-      T* st = reinterpret_cast<T*>(p.sc) + (long long)xcd_remap(blockIdx.x, gridDim.x) * kTileElems;
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          T* dst = st + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4;
-          if constexpr (sizeof(T) == 2) {
-            union { T h[4]; uint2 u; } pk;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(acc[mi][ni][r]);
-            *reinterpret_cast<uint2*>(dst) = pk.u;
-          } else {
-            *reinterpret_cast<f32x4*>(dst) = acc[mi][ni];
-          }
-        }
-    }
-    // masks -> scaled logits in log2 units (-inf where excluded). The partials cover the
-    // NEGATIVES only: self and positive are excluded (the positive logit comes from prep), so
-    // the loss is softplus(lse_neg - y_pos) with no lse - y cancellation.
-    const int col_local0 = (nt * kTile) % p.Rpad;
-    const bool own_blk = kind != kTilePlain;
-    bool cvalid[4];
-    int cloc[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      cloc[ni] = col_local0 + 64 * wn + 16 * ni + (lane & 15);
-      cvalid[ni] = cloc[ni] < p.R;
-    }
-    // Fixed-shift fast path: rows are unit-norm, so y = cos * M with M = log2(e)/tau and
-    // y - M lies in [-2M, 0]. For 2M < 120 every exp2(y - M) is a normal fp32 number, so ONE
-    // exp2 per element feeds both the row and the column partial with a common shift M (no
-    // max passes). Smaller tau falls back to per-tile max shifting (2 exps per element).
-    const bool fixed = p.fixed_shift != 0;
-    const float M = p.y_scale;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = mt * kTile + 128 * wm + 16 * mi + 4 * (lane >> 4) + r;
-        const bool rvalid = gi < p.R;
-        const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
-          if (fixed)
-            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.y_scale - M) : 0.f;
-          else
-            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
-        }
-      }
-    float2* rowred = reinterpret_cast<float2*>(smem);             // [4][256]
-    float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2][256]
-    if (fixed) {
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
-          s = row16_sum(s);
-          if ((lane & 15) == 0)
-            rowred[wn * 256 + 128 * wm + 16 * mi + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
-        }
-      if (kind == kTileSymOff) {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          float s = 0.f;
-#pragma unroll
-          for (int mi = 0; mi < 8; ++mi)
-            s += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
-          s = xrow_sum(s);
-          if ((lane >> 4) == 0) colred[wm * 256 + 64 * wn + 16 * ni + lane] = make_float2(s > 0.f ? M : kNegInf, s);
-        }
-      }
-    } else {
-    // row partials over this wave's 64 columns
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float m = fmaxf(fmaxf(acc[mi][0][r], acc[mi][1][r]), fmaxf(acc[mi][2][r], acc[mi][3][r]));
-        m = row16_max(m);
-        const float ms = (m == kNegInf) ? 0.f : m;
-        float s = fast_exp2(acc[mi][0][r] - ms) + fast_exp2(acc[mi][1][r] - ms) +
-                  fast_exp2(acc[mi][2][r] - ms) + fast_exp2(acc[mi][3][r] - ms);
-        s = row16_sum(s);
-        if ((lane & 15) == 0) rowred[wn * 256 + 128 * wm + 16 * mi + 4 * (lane >> 4) + r] = make_float2(m, s);
-      }
-    if (kind == kTileSymOff) {  // column partials = partials of the mirrored rows
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        float m = kNegInf;
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[mi][ni][r]);
-        m = xrow_max(m);
-        const float ms = (m == kNegInf) ? 0.f : m;
-        float s = 0.f;
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) s += fast_exp2(acc[mi][ni][r] - ms);
-        s = xrow_sum(s);
-        if ((lane >> 4) == 0) colred[wm * 256 + 64 * wn + 16 * ni + lane] = make_float2(m, s);
-      }
-    }
-    }  // !fixed
-    __syncthreads();
-    if (tid < 256) {
-      float2 v = rowred[tid];
-      float m = v.x, s = v.y;
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-        const float2 u = rowred[q * 256 + tid];
-        lse_merge(m, s, u.x, u.y);
-      }
-      p.part[(long long)nt * p.Rpad + mt * kTile + tid] = make_float2(m, s);
-    } else if (kind == kTileSymOff) {
-      const int c = tid - 256;
-      float2 v = colred[c];
-      float m = v.x, s = v.y;
-      const float2 u = colred[256 + c];
-      lse_merge(m, s, u.x, u.y);
-      p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
-    }
-  }
-}
-
-// Store-mode coefficient pass: read the kept cosine tile (fragment order), emit C in place.
-// Store-mode coefficient pass: one wave per 128x64 region of a kept cosine tile (fragment
-// order, 16 KiB contiguous per region) -> C into the separate coefficient buffer. 17 KiB of
-// LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound).
-template <typename T>
-__global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
-  const int lane = threadIdx.x;
-  const int idx = xcd_remap(blockIdx.x, gridDim.x);
-  const int tidx = idx >> 3, w = idx & 7;
-  const int wm = w >> 2, wn = w & 3;
-  const int4 t = p.tiles[tidx];
-  const T* st = reinterpret_cast<const T*>(p.sc) + (long long)tidx * kTileElems;
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const T* src = st + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4;
-      if constexpr (sizeof(T) == 2) {
-        union { T h[4]; u32x2 u; } pk;
-        pk.u = *reinterpret_cast<const u32x2*>(src);
-        acc[mi][ni] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
-      } else {
-        acc[mi][ni] = *reinterpret_cast<const f32x4*>(src);
-      }
-    }
-  coef_epilogue<T, 1>(acc, t.x, t.y, t.z, (lds_char*)smem, p, wm, wn, lane);
-}
 
 // ------------------------------------------------------------------------------------
 // Row prologue: one 256-thread block per positive pair (i, i+n).
@@ -486,13 +58,13 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
 template <typename Tin, typename Tc>
 __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
                                                    float* __restrict__ inv, float* __restrict__ ypos,
-                                                   int R, int d, int dk, float y_scale) {
+                                                   int R, int d, int dk, int ldk, float y_scale) {
   __shared__ float red[16];
   const int n = R >> 1, i = blockIdx.x, pi = i + n;
   const Tin* hi = h + (long long)i * d;
   const Tin* hp = h + (long long)pi * d;
-  Tc* zi = zq + (long long)i * dk;
-  Tc* zp = zq + (long long)pi * dk;
+  Tc* zi = zq + (long long)i * ldk;
+  Tc* zp = zq + (long long)pi * ldk;
   const bool vec = (d % 8) == 0;
   float ssi = 0.f, ssp = 0.f;
   if (vec) {
@@ -546,7 +118,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
 // ZqT out); the LDS tile is padded by 16 B per row.
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
-                                                        int Rpad, int dk) {
+                                                        int dk, int ldk, int ldt) {
   constexpr int V = 16 / sizeof(T);  // elements per 16 B
   constexpr int CPR = 64 / V;        // 16-B chunks per 64-element row
   __shared__ __attribute__((aligned(16))) T tile[64][64 + V];
@@ -554,7 +126,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
   for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
     const int r = k / CPR, c = k % CPR;
     u32x4 v = {0u, 0u, 0u, 0u};
-    if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * dk + e0 + c * V);
+    if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * ldk + e0 + c * V);
     *reinterpret_cast<u32x4*>(&tile[r][c * V]) = v;
   }
   __syncthreads();
@@ -563,7 +135,7 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
     union { T h[V]; u32x4 u; } pk;
 #pragma unroll
     for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][er];
-    *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * Rpad + j0 + jc * V) = pk.u;
+    *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
   }
 }
 
@@ -725,7 +297,44 @@ dev::SimParams base_params(const Geometry& g) {
   p.col_tiles = g.col_tiles;
   p.y_scale = g.inv_temp * dev::kLog2e;
   p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
+  static const int dbg = [] {
+    const char* e = std::getenv("NTXENT_GEMM_DEBUG");
+    return e ? std::atoi(e) : 0;
+  }();
+  p.dbg = dbg;
   return p;
+}
+
+// Fill the stream-K fields of `p` for `ntiles` tiles of p.kbytes each and zero the arrival
+// counters (a memset node, so the launch sequence stays graph-capturable). Returns the grid.
+int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipStream_t stream) {
+  NTXENT_CHECK(p.kbytes % kKStepBytes == 0, "K not aligned to the K step");
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  const GemmSchedule s = make_schedule(ntiles, nk, ws.num_cus);
+  p.nk = s.nk;
+  p.dp_tiles = s.dp_tiles;
+  p.sk_tiles = s.sk_tiles;
+  p.ipb = s.ipb;
+  const size_t cnt_bytes = ((size_t)ntiles * 4 + 255) / 256 * 256;
+  p.sk_cnt = static_cast<int*>(ws.ptr);
+  p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + cnt_bytes);
+  if (s.sk_tiles > 0) {
+    NTXENT_CHECK(ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
+                 "stream-K workspace too small");
+    NTXENT_HIP_CHECK(hipMemsetAsync(ws.ptr, 0, ((size_t)s.sk_tiles * 4 + 15) / 16 * 16, stream));
+  }
+  return s.grid;
+}
+
+// Leading dimension (elements) for a row of `n` elements: strides of a multiple of 1024
+// elements get 64 extra so the rows a tile streams rotate through the L2 channels.
+// NTXENT_LD_PAD overrides the pad (0 disables) for A/B measurements.
+int padded_ld(int n) {
+  static const int pad = [] {
+    const char* e = std::getenv("NTXENT_LD_PAD");
+    return e ? std::atoi(e) : 64;
+  }();
+  return (n % 1024 == 0) ? n + pad : n;
 }
 
 dev::OperandDesc rowmajor_operand(const void* base, long long ld_bytes, long long kbytes) {
@@ -750,6 +359,8 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
   g.dim = dim;
   g.dim_k = roundup(dim, 64);
   g.dim_n = roundup(dim, kTile);
+  g.ld_k = padded_ld(g.dim_k);
+  g.ld_t = padded_ld(g.rows_pad);
   g.world = world;
   g.rank = rank;
   g.row_tiles = g.rows_pad / kTile;
@@ -780,11 +391,37 @@ std::vector<int4> build_fwd_tiles(const Geometry& g) {
 }
 
 int choose_dz_ksplit(const Geometry& g, int num_cus) {
-  const int tiles = g.row_tiles * (g.dim_n / kTile);
-  const int ksteps = g.world * g.rows_pad / kTile;  // K in units of 256
-  int ks = 1;
-  while (tiles * ks < num_cus && ks * 2 <= ksteps && (ksteps % (ks * 2)) == 0) ks *= 2;
-  return ks;
+  // The persistent stream-K schedule of every similarity GEMM balances K itself, so the dZ
+  // GEMM no longer needs a split-K factor (kept for API stability; always 1).
+  (void)g;
+  (void)num_cus;
+  return 1;
+}
+
+GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
+  GemmSchedule s;
+  s.nk = nk;
+  s.grid = std::max(1, std::min(num_cus, ntiles * nk));
+  const int G = s.grid;
+  const int full = ntiles / G, rem = ntiles % G;
+  if (rem == 0) {
+    s.dp_tiles = ntiles;
+    s.sk_tiles = 0;
+  } else if (full == 0) {
+    s.dp_tiles = 0;
+    s.sk_tiles = ntiles;
+  } else {  // data-parallel rounds, then one round + the remainder shared by stream-K
+    s.dp_tiles = (full - 1) * G;
+    s.sk_tiles = ntiles - s.dp_tiles;
+  }
+  s.ipb = ((long long)s.sk_tiles * nk + G - 1) / G;
+  if (s.sk_tiles == 0) s.ipb = 0;
+  return s;
+}
+
+size_t gemm_workspace_bytes(int ntiles, int num_cus) {
+  const size_t cnt = ((size_t)ntiles * 4 + 255) / 256 * 256;
+  return cnt + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float);
 }
 
 std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit) {
@@ -800,8 +437,8 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
                  const Geometry& g, hipStream_t stream) {
   const size_t cs = dtype_size(comp);
   if (g.rows_pad > g.rows) {
-    NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq) + (size_t)g.rows * g.dim_k * cs, 0,
-                                    (size_t)(g.rows_pad - g.rows) * g.dim_k * cs, stream));
+    NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq) + (size_t)g.rows * g.ld_k * cs, 0,
+                                    (size_t)(g.rows_pad - g.rows) * g.ld_k * cs, stream));
   }
   const float ys = g.inv_temp * dev::kLog2e;
   dispatch_comp(in, [&](auto tin) {
@@ -810,7 +447,7 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
       using Tc = decltype(tc);
       hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc>), dim3(g.rows / 2), dim3(256), 0, stream,
                          static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
-                         g.dim_k, ys);
+                         g.dim_k, g.ld_k, ys);
     });
   });
   NTXENT_HIP_CHECK(hipGetLastError());
@@ -820,25 +457,28 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     hipLaunchKernelGGL((dev::transpose_kernel<Tc>), dim3(g.rows_pad / 64, g.dim_n / 64), dim3(256), 0,
-                       stream, static_cast<const Tc*>(zq), static_cast<Tc*>(zqt), g.rows_pad, g.dim_k);
+                       stream, static_cast<const Tc*>(zq), static_cast<Tc*>(zqt), g.dim_k, g.ld_k, g.ld_t);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
-                      int ntiles, float2* part, void* sc, const Geometry& g, hipStream_t stream) {
+                      int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
+                      hipStream_t stream) {
   if (ntiles == 0) return;
   const long long kb = (long long)g.dim_k * dtype_size(comp);
+  const long long ld = (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
-  p.A = rowmajor_operand(zq_local, kb, kb);
-  p.B = rowmajor_operand(zq_all, kb, kb);
+  p.A = rowmajor_operand(zq_local, ld, kb);
+  p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;
   p.kbytes = kb;
   p.part = part;
   p.sc = static_cast<char*>(sc);
+  const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeFwd>), dim3(ntiles), dim3(kGemmThreads), 0,
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeFwd>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
@@ -846,20 +486,22 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
 
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
-                      const Geometry& g, hipStream_t stream) {
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   const long long kb = (long long)g.dim_k * dtype_size(comp);
+  const long long ld = (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
-  p.A = rowmajor_operand(zq_local, kb, kb);
-  p.B = rowmajor_operand(zq_all, kb, kb);
+  p.A = rowmajor_operand(zq_local, ld, kb);
+  p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;
   p.kbytes = kb;
   p.cbuf = static_cast<char*>(cbuf);
   p.lse2 = lse2_all;
   p.cpos = cpos;
+  const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeCoef>), dim3(ntiles), dim3(kGemmThreads), 0,
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeCoef>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
@@ -893,7 +535,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 }
 
 void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
-               int ksplit, float* slabs, const Geometry& g, hipStream_t stream) {
+               float* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
   const long long cs = (long long)dtype_size(comp);
   dev::SimParams p = base_params(g);
@@ -904,21 +546,21 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.A.row_tile_stride = (long long)g.col_tiles * kTileElems * cs;
   p.A.kblk = kTile * cs;
   p.A.kblk_stride = kTileElems * cs;
-  // B = ZqT_all [W][dim_n][Rpad]: rows = embedding dims, K = global columns, one K block per rank.
+  // B = ZqT_all [W][dim_n][ld_t]: rows = embedding dims, K = global columns, one K block per rank.
   p.B.base = static_cast<const char*>(zqt_all);
-  p.B.ld = (long long)g.rows_pad * cs;
-  p.B.row_tile_stride = (long long)kTile * g.rows_pad * cs;
+  p.B.ld = (long long)g.ld_t * cs;
+  p.B.row_tile_stride = (long long)kTile * g.ld_t * cs;
   p.B.kblk = (long long)g.rows_pad * cs;
-  p.B.kblk_stride = (long long)g.dim_n * g.rows_pad * cs;
+  p.B.kblk_stride = (long long)g.dim_n * g.ld_t * cs;
   p.tiles = tiles;
-  p.kbytes = (long long)g.world * g.rows_pad * cs / ksplit;
-  NTXENT_CHECK(p.kbytes % kKStepBytes == 0, "dz split not aligned to the K step");
+  p.kbytes = (long long)g.world * g.rows_pad * cs;
   p.out = slabs;
   p.ldo = g.dim_n;
   p.slab_stride = (long long)g.rows_pad * g.dim_n;
+  const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeDz>), dim3(ntiles), dim3(kGemmThreads), 0,
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeDz>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());

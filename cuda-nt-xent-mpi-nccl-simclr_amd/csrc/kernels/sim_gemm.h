@@ -1,0 +1,646 @@
+// The NT-Xent similarity GEMM for gfx950 and its fused epilogues.
+//
+//   out tile (256 x 256) = A_tile (256 x K) * B_tile (256 x K)^T, both operands K-contiguous.
+//
+// Workgroup = 8 wave64s. K advances in 128-byte steps (64 fp16/bf16 or 32 fp32 per row).
+// LDS holds two K-steps (even/odd buffer) of A and B, each split into two 128-row halves
+// (A0, A1, B0, B1: 16 KiB each), filled by global_load_lds_dwordx4 (lane-linear
+// destination; the bank swizzle phys_chunk = chunk ^ ((row>>1)&7) is applied on the source
+// address and on the ds_read_b128 side, conflict-free for the 16x16x32 operand lane groups).
+//
+// Main loop: every K-step is 4 phases, one per 128x128 C-quadrant (A0B0, A0B1, A1B0, A1B1);
+// in each phase all 8 waves compute 64x32 of that quadrant (16 MFMA 16x16x32 per wave). A
+// half-tile is re-staged as soon as its last LDS read is one barrier behind, so loads run
+// ~1.75 K-steps ahead; every wait is a counted `s_waitcnt vmcnt(10)` (5 half-tiles still in
+// flight) followed by a raw s_barrier — no vmcnt(0) drains in the loop
+// (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4).
+//
+// Accumulator acc[mi][ni] (mi < 8, ni < 4) covers tile rows rbase(mi)..+15 and columns
+// cbase(ni)..+15 with rbase(mi) = 128(mi>>2) + 64 wa + 16(mi&3), cbase(ni) = 128(ni>>1) +
+// 32 wb + 16(ni&1) for wave w = 4 wa + wb. Kept cosine tiles use a canonical fragment order
+// (16x16 block (rb, cb) at ((rb*16 + cb)*64 + lane)*4) so producers and consumers with
+// different wave layouts agree.
+#pragma once
+
+#include "../include/ntxent/ntxent.h"
+#include "device_common.h"
+
+namespace ntxent {
+namespace dev {
+
+enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
+
+constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 64 KiB
+constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
+constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
+constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
+constexpr int kCoefWaveLds = 64 * (128 * 2 + 16);     // 17 KiB: C^T of one 128x64 region
+constexpr int kHalfBytes = 128 * kKStepBytes;         // one half-tile of one operand = 16 KiB
+
+struct OperandDesc {
+  const char* base;            // bytes
+  long long row_tile_stride;   // bytes between consecutive 256-row tiles
+  long long ld;                // bytes between rows inside a tile
+  long long kblk;              // K bytes per contiguous K block
+  long long kblk_stride;       // bytes between K blocks
+};
+
+struct SimParams {
+  OperandDesc A, B;
+  const int4* tiles;
+  long long kbytes;      // K bytes handled by one workgroup
+  int R, Rpad, n_half, own0, row_tile0, col_tiles;
+  float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
+  int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
+  float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
+  char* sc;              // kept cosines: [n_fwd_tiles][256*256] (canonical fragment order)
+  char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
+  const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
+  const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
+  float* out;            // dZ slabs
+  long long ldo;         // elements
+  long long slab_stride; // elements
+  int dbg;               // diagnostic ablations (NTXENT_GEMM_DEBUG; 0 in production)
+  // persistent stream-K schedule (see sim_gemm_kernel)
+  int nk;                // K-steps per tile
+  int dp_tiles;          // whole-tile items processed in rounds of gridDim
+  int sk_tiles;          // tiles whose K-steps are split evenly over the grid
+  long long ipb;         // stream-K K-steps per block
+  float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
+  int* sk_cnt;           // [sk_tiles] arrival counters (zeroed before every launch)
+};
+
+// Ablation bits (timing experiments only; results are garbage when set).
+constexpr int kDbgNoLoads = 1;     // skip the global->LDS staging in the main loop
+constexpr int kDbgNoStore = 2;     // forward: skip keeping the cosine tile
+constexpr int kDbgNoEpilogue = 4;  // skip every epilogue (accumulators kept live)
+
+// One monotonically advancing K position of a staged half-tile stream (clamped at the last
+// K-step, so the trailing prefetches of the schedule re-read valid memory).
+struct KStream {
+  long long kin, kbo;
+  int left;
+  __device__ __forceinline__ void init(long long k0, const OperandDesc& o, int nk) {
+    kin = k0 % o.kblk;
+    kbo = (k0 / o.kblk) * o.kblk_stride;
+    left = nk - 1;
+  }
+  __device__ __forceinline__ void advance(const OperandDesc& o) {
+    if (left > 0) {
+      --left;
+      kin += kKStepBytes;
+      if (kin == o.kblk) { kin = 0; kbo += o.kblk_stride; }
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------
+// Coefficient epilogue shared by the store-mode coef kernel (NW = 1: one wave, a 128x64
+// region at (row_base, col_base)) and the recompute GEMM (NW = 8: the whole tile).
+//   C_ij = 2^(y - lse2_i) + 2^(y - lse2_j), C_ip = cpos_i, 0 on the diagonal / padding,
+// staged transposed in LDS, then written row-major into slot (mt, nt) with 16-B stores
+// (rows via ds_read_b64_tr_b16) and, for a mirrored tile, into the lower-triangular slot.
+// ------------------------------------------------------------------------------------
+template <typename T, int NW>
+__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb)[8], const int (&cb)[4],
+                                              int row_base, int col_base, int mt, int nt, int kind,
+                                              lds_char* lds, const SimParams& p, int lane) {
+  constexpr int NROWS = NW == 8 ? kTile : 128;
+  constexpr int NCOLS = NW == 8 ? kTile : 64;
+  constexpr int S = NROWS * 2 + 16;  // LDS row stride (bytes) of the C^T staging tile
+  constexpr int NT = NW * 64;        // threads in the calling block
+  T* base = reinterpret_cast<T*>(p.cbuf);
+  const int col_local0 = (nt * kTile) % p.Rpad;  // rank-local column of this tile's col 0
+  // Fixed-shift form (2M < 120, see the forward epilogue):
+  // C = 2^(y - M) * (2^(M - lse2_i) + 2^(M - lse2_j)), one exp2 per element.
+  const bool fixed = p.fixed_shift != 0;
+  const float M = p.y_scale;
+  float lcol[4];
+  bool cvalid[4];
+  int gj[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col_t = cb[ni] + (lane & 15);
+    gj[ni] = nt * kTile + col_t;
+    const float l = p.lse2[gj[ni]];
+    lcol[ni] = fixed ? fast_exp2(M - l) : l;
+    cvalid[ni] = (col_local0 + col_t) < p.R;
+  }
+  T* slot = base + ((long long)mt * p.col_tiles + nt) * kTileElems;
+  T* mirror = nullptr;
+  if (kind == kTileSymOff)
+    mirror = base + ((long long)(nt - p.row_tile0) * p.col_tiles + p.row_tile0 + mt) * kTileElems;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    float c[4][4];
+    const int row_t0 = rb[mi] + 4 * (lane >> 4);
+    const int gi0 = mt * kTile + row_t0;  // 4 consecutive rows
+    const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
+    const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int gi = gi0 + r;
+      const bool rvalid = gi < p.R;
+      const float lrow = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
+      const int gself = p.own0 + gi;
+      const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const float y = acc[mi][ni][r] * p.y_scale;
+        float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
+        v = (gj[ni] == gpos) ? cpos4[r] : v;  // positive: -(a_i + a_p), no 1 - P cancellation
+        v = (rvalid && cvalid[ni] && gj[ni] != gself) ? v : 0.0f;
+        c[ni][r] = v;
+      }
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col_t = cb[ni] + (lane & 15);
+      if constexpr (sizeof(T) == 2) {
+        // stage C^T in LDS: Ct[col][row0..row0+3] (one ds_write_b64 per fragment)
+        union { T h[4]; u32x2 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(c[ni][r]);
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(lds + (col_t - col_base) * S +
+                                                                     (row_t0 - row_base) * 2) = pk.u;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) slot[(row_t0 + r) * kTile + col_t] = c[ni][r];
+        if (mirror)
+          *reinterpret_cast<f32x4*>(mirror + col_t * kTile + row_t0) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
+      }
+    }
+  }
+  if constexpr (sizeof(T) == 2) {
+    __syncthreads();
+    const int tid = threadIdx.x, w = tid >> 6;  // w = wave index inside the calling block
+    // (a) mirrored tile: Ct rows are rows of C^T -> coalesced 16-B stores into the mirror slot.
+    if (mirror) {
+      constexpr int CPR = NROWS * 2 / 16;  // 16-B chunks per staged row
+#pragma unroll 4
+      for (int q = 0; q < NCOLS * CPR / NT; ++q) {
+        const int k = tid + NT * q;
+        const int row = k / CPR, c16 = k % CPR;
+        const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(mirror) + (col_base + row) * (kTile * 2) + row_base * 2 +
+                                  c16 * 16) = v;
+      }
+    }
+    // (b) rows of C = columns of Ct via the gfx950 transposed LDS read (ds_read_b64_tr_b16):
+    //     a 16-lane group reads a 4 (Ct rows) x 16 (Ct cols) block and lane i receives column
+    //     i, i.e. 4 consecutive entries of C row c0+i. Two reads give 16 B per lane.
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    constexpr int RB = NROWS / 16;                // 16-row blocks of C in this call
+    constexpr int NBLK = RB * (NCOLS / 32) / NW;  // 16x32 blocks per wave (= 16)
+    const int g = lane >> 4, i = lane & 15, q4 = i >> 2, p4 = i & 3;
+#pragma unroll 2
+    for (int b = 0; b < NBLK; ++b) {
+      const int blk = w * NBLK + b;
+      const int c0 = (blk % RB) * 16;  // C rows row_base+c0 .. +15
+      const int r0 = (blk / RB) * 32 + 8 * g;  // C cols col_base+r0 .. +7
+      const lds_char* a0 = lds + (r0 + q4) * S + (c0 + 4 * p4) * 2;
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * S));
+      u32x4 u;
+      u[0] = (unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
+      u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
+      u[2] = (unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
+      u[3] = (unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
+                                (col_base + r0) * 2) = u;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// The similarity GEMM with its three epilogues (see the file header for the schedule).
+// ------------------------------------------------------------------------------------
+template <typename T, int MODE>
+__global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
+  typedef typename Mfma<T>::frag frag;
+  typedef __attribute__((address_space(3))) const frag lds_frag;
+  __shared__ __attribute__((aligned(16))) char smem[MODE == kModeCoef ? kCoefLds : kGemmLds];
+  lds_char* lds = (lds_char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wa = w >> 2, wb = w & 3;
+  const int G = gridDim.x;
+  const int bid = xcd_remap(blockIdx.x, G);  // persistent block id (XCD-contiguous runs)
+  const int nk = p.nk;                       // K-steps of a whole tile
+  const char* Ab = nullptr;
+  const char* Bb = nullptr;
+  KStream sa0, sa1, sb0, sb1;
+
+  // per-lane source offsets of this wave's two 8-row pieces of each half-tile
+  unsigned a_off[2][2], b_off[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 128 * h + 16 * w + 8 * j + (lane >> 3);
+      const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
+      a_off[h][j] = (unsigned)(row * p.A.ld) + lchunk * 16;
+      b_off[h][j] = (unsigned)(row * p.B.ld) + lchunk * 16;
+    }
+  // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
+  auto stage = [&](int isB, int h, KStream& s, int buf) {
+    lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
+    const char* src = (isB ? Bb : Ab) + s.kbo + s.kin;
+    if (!(p.dbg & kDbgNoLoads)) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
+                                         (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, 0);
+    }
+    s.advance(isB ? p.B : p.A);
+  };
+
+  f32x4 acc[8][4];
+
+  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
+  frag af[2][4], bf0[2][2], bf1[2][2];  // [k-substep][block]
+  auto read_a = [&](int buf, int h, frag (&af)[2][4]) {
+    const lds_char* As = lds + buf * kStageBytes;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int pch = ((4 * s + cq) ^ sw) << 4;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+        af[s][mi] = *(lds_frag*)(As + (128 * h + 64 * wa + 16 * mi + r16) * kKStepBytes + pch);
+    }
+  };
+  auto read_b = [&](int buf, int h, frag (&bf)[2][2]) {
+    const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int pch = ((4 * s + cq) ^ sw) << 4;
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+        bf[s][ni] = *(lds_frag*)(Bs + (128 * h + 32 * wb + 16 * ni + r16) * kKStepBytes + pch);
+    }
+  };
+  // s_setprio(1)/(0) around each MFMA cluster keeps hipcc from sinking the cluster across the
+  // next s_barrier (cdna_hip_programming.md §5.5 T5).
+  auto mma_quadrant = [&](int qa, int qb, frag (&af)[2][4], frag (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
+          c = (MODE == kModeDz) ? Mfma<T>::mma(bf[s][ni], af[s][mi], c) : Mfma<T>::mma(af[s][mi], bf[s][ni], c);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto lds_drain = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
+  // phase has retired for this wave (4 younger half-tiles may stay in flight).
+  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  // Wave group (0: waves 0-3, 1: waves 4-7); each SIMD hosts one wave of each group.
+  const int grp = __builtin_amdgcn_readfirstlane(w) >> 2;
+
+  // Each K-step: 4 phases (C-quadrants), each split into a load interval L (re-stage one
+  // half-tile, read this phase's operands into registers, drain the reads) and a compute
+  // interval C (16 MFMA from registers), separated by barriers. Group 1 runs one barrier
+  // behind group 0 (staggered ping-pong), so on every SIMD one wave's L overlaps its partner's
+  // C and the MFMA pipe alternates between them (cdna_hip_programming.md §5, 8-phase).
+  //   phase 1: stage A1(t+1) | read A0(t) B0(t) | MFMA A0B0
+  //   phase 2: stage A0(t+2) | read B1(t)       | MFMA A0B1
+  //   phase 3: stage B0(t+2) | read A1(t)       | MFMA A1B0
+  //   phase 4: stage B1(t+2) |                  | MFMA A1B1
+  // Correctness under the stagger: a half-tile is re-staged one phase after its last read,
+  // and every read drains (lgkmcnt) before the next barrier, so the other group has finished
+  // reading it (WAR); DMA waits run one phase ahead, so both groups' copies of a half-tile
+  // retired before a barrier that precedes either group's read (RAW).
+  //
+  // Persistent stream-K schedule: the first dp_tiles tiles are whole-tile work items
+  // (rounds of G); the remaining sk_tiles * nk K-steps are split evenly (ipb steps per block).
+  // A tile split across blocks is finished by its last-arriving block (fixup below).
+  const long long sk_total = (long long)p.sk_tiles * nk;
+  const long long it0 = (long long)bid * p.ipb;
+  const long long it1 = it0 + p.ipb < sk_total ? it0 + p.ipb : sk_total;
+  const int n_dp = p.dp_tiles > bid ? (p.dp_tiles - bid + G - 1) / G : 0;
+  long long it = it0;
+  for (int item = 0;; ++item) {
+  int tile, kb, ke, stile = -1;
+  long long seg0 = 0;
+  if (item < n_dp) {
+    tile = bid + item * G;
+    kb = 0;
+    ke = nk;
+  } else {
+    if (it >= it1) break;
+    stile = (int)(it / nk);
+    kb = (int)(it % nk);
+    ke = (int)((long long)kb + (it1 - it) < nk ? kb + (it1 - it) : nk);
+    seg0 = it;
+    it += ke - kb;
+    tile = p.dp_tiles + stile;
+  }
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y;
+  const int nsteps = ke - kb;
+  Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
+  Bb = p.B.base + (long long)nt * p.B.row_tile_stride;
+  {
+    const long long k0 = (long long)kb * kKStepBytes;
+    sa0.init(k0, p.A, nsteps); sa1.init(k0, p.A, nsteps);
+    sb0.init(k0, p.B, nsteps); sb1.init(k0, p.B, nsteps);
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1 (the stream clamps keep the
+  // trailing prefetches in bounds, so every wait count below is uniform)
+  stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
+  stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
+  barrier();
+  if (grp == 1) barrier();  // stagger group 1 by one barrier
+  for (int ks = 0; ks < nsteps; ++ks) {
+    const int cur = ks & 1, nxt = cur ^ 1;
+    dma_wait(); barrier();          // phase 1 L (wait covers B1(t) for phase 2)
+    stage(0, 1, sa1, nxt);          //   A1 of step ks+1
+    read_a(cur, 0, af);
+    read_b(cur, 0, bf0);
+    lds_drain(); barrier();         // phase 1 C
+    mma_quadrant(0, 0, af, bf0);
+    dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
+    stage(0, 0, sa0, cur);          //   A0 of step ks+2
+    read_b(cur, 1, bf1);
+    lds_drain(); barrier();         // phase 2 C
+    mma_quadrant(0, 1, af, bf1);
+    barrier();                      // phase 3 L
+    stage(1, 0, sb0, cur);          //   B0 of step ks+2
+    read_a(cur, 1, af);
+    lds_drain(); barrier();         // phase 3 C
+    mma_quadrant(1, 0, af, bf0);
+    dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
+    stage(1, 1, sb1, cur);          //   B1 of step ks+2
+    barrier();                      // phase 4 C
+    mma_quadrant(1, 1, af, bf1);
+  }
+  if (grp == 0) barrier();  // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
+  __syncthreads();
+  {
+  // Thread indices re-derived through an opaque copy: keeps the compiler from hoisting the
+  // epilogue's address arithmetic out of the persistent loop, where it would stay live across
+  // the MFMA main loop and spill.
+  int tid_e = threadIdx.x;
+  asm volatile("" : "+v"(tid_e));
+  const int tid = tid_e, lane = tid_e & 63, w = tid_e >> 6;
+  const int wa = w >> 2, wb = w & 3;
+  int rb[8], cb[4];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) rb[mi] = 128 * (mi >> 2) + 64 * wa + 16 * (mi & 3);
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) cb[ni] = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
+
+  if (nsteps != nk) {
+    // ---- stream-K fixup: partial K-range of tile `stile` -------------------------------
+    // Publish the fp32 partial (canonical fragment order, 256 KiB) with plain stores, drain,
+    // agent-scope release, then count arrivals (cdna_hip_programming.md §5, split-K recipe).
+    // The last arriver acquires and re-sums ALL segments in block order (deterministic).
+    const int b0 = (int)((long long)stile * nk / p.ipb);
+    const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
+    auto slot_of = [&](int bb) {
+      const long long s = (long long)bb * p.ipb;
+      const bool first_partial = (s / nk == stile) && (s % nk != 0);
+      return p.sk_slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
+    };
+    (void)seg0;
+    float* mine = slot_of(bid);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        *reinterpret_cast<f32x4*>(mine + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4) = acc[mi][ni];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == b1 - b0;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    const bool last = flag[0] != 0;
+    __syncthreads();
+    if (!last) continue;
+    for (int bb = b0; bb <= b1; ++bb) {
+      const float* src = slot_of(bb);
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4);
+          acc[mi][ni] = (bb == b0) ? v : acc[mi][ni] + v;
+        }
+    }
+  }
+
+  if (p.dbg & kDbgNoEpilogue) {  // timing ablation: keep the MFMA results live, write nothing
+    float s = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) s += acc[mi][ni][0] + acc[mi][ni][3];
+    if (s == 1.2345e-30f) p.part[tid] = make_float2(s, s);
+  } else if constexpr (MODE == kModeDz) {
+    // swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r]
+    float* out = p.out;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const long long row = (long long)mt * kTile + rb[mi] + (lane & 15);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = nt * kTile + cb[ni] + 4 * (lane >> 4);
+        *reinterpret_cast<f32x4*>(out + row * p.ldo + col) = acc[mi][ni];
+      }
+    }
+  } else if constexpr (MODE == kModeCoef) {
+    coef_epilogue<T, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
+  } else {
+    const int kind = t.z;
+    if (p.sc && !(p.dbg & kDbgNoStore)) {  // keep cosines (compact slot per tile, canonical order)
+      T* st = reinterpret_cast<T*>(p.sc) + (long long)tile * kTileElems;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          T* dst = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
+          if constexpr (sizeof(T) == 2) {
+            union { T h[4]; u32x2 u; } pk;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(acc[mi][ni][r]);
+            *reinterpret_cast<u32x2*>(dst) = pk.u;
+          } else {
+            *reinterpret_cast<f32x4*>(dst) = acc[mi][ni];
+          }
+        }
+    }
+    // masks -> scaled logits in log2 units. The partials cover the NEGATIVES only: self and
+    // positive are excluded (the positive logit comes from prep), so the loss is
+    // softplus(lse_neg - y_pos) with no lse - y cancellation.
+    // Fixed-shift fast path: rows are unit-norm, so y = cos * M with M = log2(e)/tau and
+    // y - M lies in [-2M, 0]. For 2M < 120 every exp2(y - M) is a normal fp32 number, so ONE
+    // exp2 per element feeds both the row and the column partial with a common shift M (no
+    // max passes). Smaller tau falls back to per-tile max shifting (2 exps per element).
+    const int col_local0 = (nt * kTile) % p.Rpad;
+    const bool own_blk = kind != kTilePlain;
+    const bool fixed = p.fixed_shift != 0;
+    const float M = p.y_scale;
+    bool cvalid[4];
+    int cloc[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      cloc[ni] = col_local0 + cb[ni] + (lane & 15);
+      cvalid[ni] = cloc[ni] < p.R;
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = mt * kTile + rb[mi] + 4 * (lane >> 4) + r;
+        const bool rvalid = gi < p.R;
+        const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
+          if (fixed)
+            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.y_scale - M) : 0.f;
+          else
+            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
+        }
+      }
+    float2* rowred = reinterpret_cast<float2*>(smem);                // [4 wb][256]
+    float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2 wa][256]
+    if (fixed) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
+          s = row16_sum(s);
+          if ((lane & 15) == 0)
+            rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
+        }
+      if (kind == kTileSymOff) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          float s = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+            s += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
+          s = xrow_sum(s);
+          if ((lane >> 4) == 0) colred[wa * 256 + cb[ni] + lane] = make_float2(s > 0.f ? M : kNegInf, s);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float m = fmaxf(fmaxf(acc[mi][0][r], acc[mi][1][r]), fmaxf(acc[mi][2][r], acc[mi][3][r]));
+          m = row16_max(m);
+          const float ms = (m == kNegInf) ? 0.f : m;
+          float s = fast_exp2(acc[mi][0][r] - ms) + fast_exp2(acc[mi][1][r] - ms) +
+                    fast_exp2(acc[mi][2][r] - ms) + fast_exp2(acc[mi][3][r] - ms);
+          s = row16_sum(s);
+          if ((lane & 15) == 0) rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(m, s);
+        }
+      if (kind == kTileSymOff) {  // column partials = partials of the mirrored rows
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          float m = kNegInf;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[mi][ni][r]);
+          m = xrow_max(m);
+          const float ms = (m == kNegInf) ? 0.f : m;
+          float s = 0.f;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += fast_exp2(acc[mi][ni][r] - ms);
+          s = xrow_sum(s);
+          if ((lane >> 4) == 0) colred[wa * 256 + cb[ni] + lane] = make_float2(m, s);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      float2 v = rowred[tid];
+      float m = v.x, s = v.y;
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float2 u = rowred[q * 256 + tid];
+        lse_merge(m, s, u.x, u.y);
+      }
+      p.part[(long long)nt * p.Rpad + mt * kTile + tid] = make_float2(m, s);
+    } else if (kind == kTileSymOff) {
+      const int c = tid - 256;
+      float2 v = colred[c];
+      float m = v.x, s = v.y;
+      const float2 u = colred[256 + c];
+      lse_merge(m, s, u.x, u.y);
+      p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
+    }
+  }
+  }  // epilogue scope
+  __syncthreads();  // LDS of this item's epilogue is reused by the next item's staging
+  }  // work items
+}
+
+// Store-mode coefficient pass: one wave per 128x64 region (wm, wn) of a kept cosine tile
+// (canonical fragment order: 32 fragments of 512 B) -> C into the coefficient buffer. 17 KiB
+// of LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound).
+template <typename T>
+__global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
+  const int lane = threadIdx.x;
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);
+  const int tidx = idx >> 3, w = idx & 7;
+  const int wm = w >> 2, wn = w & 3;
+  const int4 t = p.tiles[tidx];
+  const T* st = reinterpret_cast<const T*>(p.sc) + (long long)tidx * kTileElems;
+  int rb[8], cb[4];
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) rb[mi] = 128 * wm + 16 * mi;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) cb[ni] = 64 * wn + 16 * ni;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const T* src = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
+      if constexpr (sizeof(T) == 2) {
+        union { T h[4]; u32x2 u; } pk;
+        pk.u = *reinterpret_cast<const u32x2*>(src);
+        acc[mi][ni] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
+      } else {
+        acc[mi][ni] = *reinterpret_cast<const f32x4*>(src);
+      }
+    }
+  coef_epilogue<T, 1>(acc, rb, cb, 128 * wm, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+}
+
+}  // namespace dev
+}  // namespace ntxent

@@ -58,11 +58,14 @@ struct Plan {
   at::Tensor dz_tiles;
   int n_dz = 0;
   int ksplit = 1;
+  int num_cus = 256;
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
   int dim() const { return g.dim; }
   int dim_k() const { return g.dim_k; }
+  int ld_k() const { return g.ld_k; }
+  int ld_t() const { return g.ld_t; }
   int dim_n() const { return g.dim_n; }
   int world() const { return g.world; }
   int rank() const { return g.rank; }
@@ -92,6 +95,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->comp = comp;
   p->device = device;
   const DeviceInfo& di = device_info(device);
+  p->num_cus = di.num_cus;
   auto ft = build_fwd_tiles(p->g);
   p->n_fwd = (int)ft.size();
   p->fwd_tiles = upload_tiles(ft, device);
@@ -116,12 +120,23 @@ static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
   return at::TensorOptions().dtype(t).device(like.device());
 }
 
+// Stream-K scratch for one GEMM launch, from the caching allocator (released with the
+// returned tensor once the stream has consumed it).
+static std::pair<at::Tensor, GemmWorkspace> gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
+  GemmWorkspace ws;
+  ws.num_cus = P.num_cus;
+  ws.bytes = gemm_workspace_bytes(ntiles, P.num_cus);
+  auto t = at::empty({(long)ws.bytes}, opts(like, at::kByte));
+  ws.ptr = t.data_ptr();
+  return {t, ws};
+}
+
 // ---- stage ops ----------------------------------------------------------------------
 std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
   const at::DeviceGuard guard(h.device());
-  auto zq = at::empty({P.g.rows_pad, P.g.dim_k}, opts(h, to_scalar(P.comp)));
+  auto zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.comp)));
   auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
   auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
   launch_prep(to_dtype(h.scalar_type()), P.comp, h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(),
@@ -132,7 +147,7 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
 at::Tensor transpose(const at::Tensor& zq, const Plan& P) {
   check_input(zq, "zq");
   const at::DeviceGuard guard(zq.device());
-  auto zqt = at::empty({P.g.dim_n, P.g.rows_pad}, zq.options());
+  auto zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
   launch_transpose(P.comp, zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
 }
@@ -141,16 +156,17 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
                                   bool keep_cos) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
-  NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.g.dim_k,
-               "zq_all must be [world*rows_pad, dim_k]");
+  NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.g.ld_k,
+               "zq_all must be [world*rows_pad, ld_k]");
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
   if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, zq_local.options());
+  auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
-                   P.g, cur_stream(zq_local));
+                   ws.second, P.g, cur_stream(zq_local));
   return {part, sc};
 }
 
@@ -187,20 +203,22 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
-                   P.g, cur_stream(zq_local));
+                   ws.second, P.g, cur_stream(zq_local));
   return cbuf;
 }
 
 at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   check_input(sc, "sc");
   check_input(zqt_all, "zqt_all");
-  NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.rows_pad, "zqt_all must be [world, dim_n, rows_pad]");
+  NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
   const at::DeviceGuard guard(sc.device());
   auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
+  auto ws = gemm_ws(sc, P.n_dz, P);
   launch_dz(P.comp, sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
-            P.n_dz, P.ksplit, slabs.data_ptr<float>(), P.g, cur_stream(sc));
+            P.n_dz, slabs.data_ptr<float>(), ws.second, P.g, cur_stream(sc));
   return slabs;
 }
 
@@ -344,6 +362,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("rows_pad", &Plan::rows_pad)
       .def_property_readonly("dim", &Plan::dim)
       .def_property_readonly("dim_k", &Plan::dim_k)
+      .def_property_readonly("ld_k", &Plan::ld_k)
+      .def_property_readonly("ld_t", &Plan::ld_t)
       .def_property_readonly("dim_n", &Plan::dim_n)
       .def_property_readonly("world", &Plan::world)
       .def_property_readonly("rank", &Plan::rank)

@@ -44,9 +44,9 @@ class DistNTXentFunction(torch.autograd.Function):
         plan = C.get_plan(R, d, W, r, float(temperature), compute, h.device.index)
         zq, inv, ypos = C.prep(h, plan)
         Rpad = plan.rows_pad
-        zq_all = torch.empty((W * Rpad, plan.dim_k), dtype=zq.dtype, device=h.device)
+        zq_all = torch.empty((W * Rpad, plan.ld_k), dtype=zq.dtype, device=h.device)
         zqt = C.transpose(zq, plan)
-        zqt_all = torch.empty((W, plan.dim_n, Rpad), dtype=zq.dtype, device=h.device)
+        zqt_all = torch.empty((W, plan.dim_n, plan.ld_t), dtype=zq.dtype, device=h.device)
         if W > 1:
             work_z = dist.all_gather_into_tensor(zq_all, zq, group=group, async_op=overlap)
             work_t = dist.all_gather_into_tensor(zqt_all, zqt, group=group, async_op=True)
