@@ -412,5 +412,35 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     r["is_gfx950"] = d.is_gfx950;
     return r;
   });
+  // host-only planning helpers (no device needed: unit-tested on CPU)
+  m.def("geometry", [](int rows, int dim, int world, int rank, double T) {
+    const auto g = ntxent::make_geometry(rows, dim, world, rank, (float)T);
+    py::dict r;
+    r["rows"] = g.rows; r["rows_pad"] = g.rows_pad; r["dim"] = g.dim; r["dim_k"] = g.dim_k;
+    r["dim_n"] = g.dim_n; r["ld_k"] = g.ld_k; r["ld_t"] = g.ld_t; r["world"] = g.world;
+    r["rank"] = g.rank; r["row_tiles"] = g.row_tiles; r["col_tiles"] = g.col_tiles;
+    r["global_rows"] = g.global_rows;
+    return r;
+  }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0, py::arg("T") = 0.07);
+  auto tiles_to_list = [](const std::vector<int4>& v) {
+    py::list l;
+    for (const auto& t : v) l.append(py::make_tuple(t.x, t.y, t.z));
+    return l;
+  };
+  m.def("fwd_tile_list", [tiles_to_list](int rows, int dim, int world, int rank) {
+    return tiles_to_list(ntxent::build_fwd_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f)));
+  }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
+  m.def("dz_tile_list", [tiles_to_list](int rows, int dim, int world, int rank) {
+    return tiles_to_list(ntxent::build_dz_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), 1));
+  }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
+  m.def("schedule", [](int ntiles, int nk, int num_cus) {
+    const auto s = ntxent::make_schedule(ntiles, nk, num_cus);
+    py::dict r;
+    r["grid"] = s.grid; r["nk"] = s.nk; r["dp_tiles"] = s.dp_tiles; r["sk_tiles"] = s.sk_tiles;
+    r["ipb"] = s.ipb;
+    return r;
+  }, py::arg("ntiles"), py::arg("nk"), py::arg("num_cus"));
+  m.def("gemm_workspace_bytes", &ntxent::gemm_workspace_bytes);
   m.attr("TILE") = ntxent::kTile;
+  m.attr("K_STEP_BYTES") = ntxent::kKStepBytes;
 }

@@ -1,0 +1,94 @@
+"""Host-side planning logic of the HIP path (runs on CPU: no device needed).
+
+Checks the invariants the kernels rely on: the forward tile list covers every (row, column)
+tile pair exactly once counting the mirrored lower triangle of the own-rank block, the dZ
+tiles cover the output, and the persistent stream-K schedule covers every K-step of every
+tile exactly once with the per-block work balanced.
+"""
+import pytest
+
+from ntxent_amd.ops import _ext
+
+
+@pytest.fixture(scope="module")
+def C():
+    return _ext.load()
+
+
+@pytest.mark.parametrize("rows,dim", [(64, 128), (34, 100), (8192, 2048), (600, 200), (2048, 8192)])
+def test_geometry(C, rows, dim):
+    g = C.geometry(rows, dim)
+    assert g["rows_pad"] % C.TILE == 0 and g["rows_pad"] >= rows > g["rows_pad"] - C.TILE
+    assert g["dim_k"] % 64 == 0 and g["dim_k"] >= dim
+    assert g["dim_n"] % C.TILE == 0 and g["dim_n"] >= g["dim_k"]
+    assert g["ld_k"] >= g["dim_k"] and g["ld_t"] >= g["rows_pad"]
+    # de-aliased strides: never a multiple of 1024 elements
+    assert g["ld_k"] % 1024 != 0 and g["ld_t"] % 1024 != 0
+    assert g["col_tiles"] == g["row_tiles"] and g["global_rows"] == rows
+
+
+def test_geometry_rejects_bad_input(C):
+    with pytest.raises(Exception):
+        C.geometry(7, 16)
+    with pytest.raises(Exception):
+        C.geometry(8, 16, 2, 2)
+    with pytest.raises(Exception):
+        C.geometry(8, 0)
+
+
+@pytest.mark.parametrize("rows,world,rank", [(512, 1, 0), (8192, 1, 0), (1024, 4, 2), (300, 2, 1), (8192, 8, 7)])
+def test_fwd_tiles_cover_once(C, rows, world, rank):
+    g = C.geometry(rows, 64, world, rank)
+    tiles = C.fwd_tile_list(rows, 64, world, rank)
+    own = rank * g["row_tiles"]
+    covered = {}
+    for ti, tj, kind in tiles:
+        local = tj - own
+        if 0 <= local < g["row_tiles"]:
+            assert local >= ti
+            assert kind == (1 if local == ti else 2)
+            covered[(ti, tj)] = covered.get((ti, tj), 0) + 1
+            if local != ti:
+                covered[(local, own + ti)] = covered.get((local, own + ti), 0) + 1
+        else:
+            assert kind == 0
+            covered[(ti, tj)] = covered.get((ti, tj), 0) + 1
+    assert len(covered) == g["row_tiles"] * g["col_tiles"]
+    assert set(covered.values()) == {1}
+    rt = g["row_tiles"]
+    assert len(tiles) == rt * (g["col_tiles"] - rt) + rt * (rt + 1) // 2
+
+
+def test_dz_tiles_cover_output(C):
+    g = C.geometry(1024, 600)
+    tiles = C.dz_tile_list(1024, 600)
+    assert sorted((t[0], t[1]) for t in tiles) == [(i, j) for i in range(g["row_tiles"]) for j in range(g["dim_n"] // C.TILE)]
+
+
+@pytest.mark.parametrize("ntiles,nk,cus", [(528, 32, 256), (256, 128, 256), (10, 4, 256), (1, 3, 256),
+                                           (300, 7, 256), (136, 16, 80), (1000, 2, 256)])
+def test_stream_k_schedule(C, ntiles, nk, cus):
+    s = C.schedule(ntiles, nk, cus)
+    G = s["grid"]
+    assert 1 <= G <= cus
+    assert s["dp_tiles"] + s["sk_tiles"] == ntiles
+    assert s["dp_tiles"] % G == 0  # whole data-parallel rounds
+    # every stream-K iteration is owned by exactly one block, contiguous ranges
+    total = s["sk_tiles"] * nk
+    if total:
+        ipb = s["ipb"]
+        assert G * ipb >= total and ipb == -(-total // G)  # minimal even split; tail blocks may idle
+        owned = 0
+        for b in range(G):
+            lo, hi = b * ipb, min((b + 1) * ipb, total)
+            owned += max(0, hi - lo)
+        assert owned == total
+    # balance: the busiest block does at most one DP round + ipb steps more than the mean
+    mean = ntiles * nk / G
+    worst = (s["dp_tiles"] // G) * nk + s["ipb"]
+    assert worst <= mean + nk + 1
+
+
+def test_workspace_bytes(C):
+    b = C.gemm_workspace_bytes(528, 256)
+    assert b >= 528 * 4 + 2 * 256 * 256 * 256 * 4
