@@ -15,11 +15,15 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <random>
 #include <string>
 #include <vector>
 
-#include "ntxent/ntxent.h"
+#include "ntxent/engine.h"
 
 using namespace ntxent;
 
@@ -39,27 +43,6 @@ uint16_t f32_to_f16(float f) {
   return u;
 }
 
-struct Buffers {
-  void* h = nullptr;
-  void* dh = nullptr;
-  void* zq = nullptr;
-  void* zqt = nullptr;
-  float* inv = nullptr;
-  float* ypos = nullptr;
-  float2* part = nullptr;
-  void* sbuf = nullptr;
-  void* cbuf = nullptr;
-  float* lse2 = nullptr;
-  float* cpos = nullptr;
-  float* block_loss = nullptr;
-  float* loss = nullptr;
-  float* grad_out = nullptr;
-  float* slabs = nullptr;
-  int4* fwd_tiles = nullptr;
-  int4* dz_tiles = nullptr;
-  int n_fwd = 0, n_dz = 0, ksplit = 1;
-};
-
 struct Result {
   double mean = 0, stdev = 0, mn = 0, mx = 0;
 };
@@ -77,101 +60,85 @@ Result stats(std::vector<float> v) {
   return r;
 }
 
+// Synthetic two-view embeddings: view2 = shared basis + noise, like positives of a trained
+// encoder, so the loss is well inside (0, log(2N-1)).
+std::vector<float> synthetic_views(int rows, int dim, unsigned seed) {
+  std::mt19937 rng(seed);
+  std::normal_distribution<float> nd;
+  std::vector<float> h((size_t)rows * dim);
+  const size_t n = rows / 2;
+  for (size_t i = 0; i < n; ++i)
+    for (int e = 0; e < dim; ++e) {
+      const float b = nd(rng);
+      h[i * dim + e] = b + 0.5f * nd(rng);
+      h[(i + n) * dim + e] = b + 0.5f * nd(rng);
+    }
+  return h;
+}
+
+// Uploads `host` in dtype `in`; rounds `host` to what the device sees.
+void* upload(std::vector<float>& host, DType in) {
+  void* d = nullptr;
+  const size_t n = host.size();
+  NTXENT_HIP_CHECK(hipMalloc(&d, n * dtype_size(in)));
+  if (in == DType::F32) {
+    NTXENT_HIP_CHECK(hipMemcpy(d, host.data(), n * 4, hipMemcpyHostToDevice));
+    return d;
+  }
+  std::vector<uint16_t> h16(n);
+  for (size_t k = 0; k < n; ++k) {
+    h16[k] = in == DType::BF16 ? f32_to_bf16(host[k]) : f32_to_f16(host[k]);
+    if (in == DType::BF16) {
+      uint32_t u = (uint32_t)h16[k] << 16;
+      std::memcpy(&host[k], &u, 4);
+    } else {
+      _Float16 hh;
+      std::memcpy(&hh, &h16[k], 2);
+      host[k] = (float)hh;
+    }
+  }
+  NTXENT_HIP_CHECK(hipMemcpy(d, h16.data(), n * 2, hipMemcpyHostToDevice));
+  return d;
+}
+
 class Bench {
  public:
-  Bench(int batch, int dim, DType in, DType comp, float T, int ncus)
-      : in_(in), comp_(comp), g_(make_geometry(2 * batch, dim, 1, 0, T)) {
-    const size_t is = dtype_size(in), cs = dtype_size(comp);
-    const size_t R = g_.rows, Rp = g_.rows_pad;
-    auto ft = build_fwd_tiles(g_);
-    b_.ksplit = choose_dz_ksplit(g_, ncus);
-    auto dt = build_dz_tiles(g_, b_.ksplit);
-    b_.n_fwd = (int)ft.size();
-    b_.n_dz = (int)dt.size();
-    NTXENT_HIP_CHECK(hipMalloc(&b_.h, R * dim * is));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.dh, R * dim * is));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.zq, Rp * g_.ld_k * cs));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.zqt, (size_t)g_.dim_n * g_.ld_t * cs));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.inv, R * 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.ypos, R * 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.part, (size_t)g_.col_tiles * Rp * 8));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.sbuf, (size_t)b_.n_fwd * kTileElems * cs));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.cbuf, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.lse2, Rp * 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.cpos, Rp * 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.block_loss, Rp / 256 * 4 + 64));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.loss, 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.grad_out, 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.slabs, (size_t)b_.ksplit * Rp * g_.dim_n * 4));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.fwd_tiles, ft.size() * sizeof(int4)));
-    NTXENT_HIP_CHECK(hipMalloc(&b_.dz_tiles, dt.size() * sizeof(int4)));
-    NTXENT_HIP_CHECK(hipMemcpy(b_.fwd_tiles, ft.data(), ft.size() * sizeof(int4), hipMemcpyHostToDevice));
-    NTXENT_HIP_CHECK(hipMemcpy(b_.dz_tiles, dt.data(), dt.size() * sizeof(int4), hipMemcpyHostToDevice));
-    const float one = 1.0f;
-    NTXENT_HIP_CHECK(hipMemcpy(b_.grad_out, &one, 4, hipMemcpyHostToDevice));
-    // synthetic random-normal embeddings (two noisy views of shared bases)
-    std::mt19937 rng(1234);
-    std::normal_distribution<float> nd;
-    host_.resize(R * dim);
-    const size_t n = R / 2;
-    for (size_t i = 0; i < n; ++i)
-      for (int e = 0; e < dim; ++e) {
-        const float b = nd(rng);
-        host_[i * dim + e] = b + 0.5f * nd(rng);
-        host_[(i + n) * dim + e] = b + 0.5f * nd(rng);
-      }
-    std::vector<uint16_t> h16(R * dim);
-    if (in == DType::F32) {
-      NTXENT_HIP_CHECK(hipMemcpy(b_.h, host_.data(), R * dim * 4, hipMemcpyHostToDevice));
-    } else {
-      for (size_t k = 0; k < h16.size(); ++k) {
-        h16[k] = in == DType::BF16 ? f32_to_bf16(host_[k]) : f32_to_f16(host_[k]);
-        // keep the host copy equal to what the device sees
-        if (in == DType::BF16) {
-          uint32_t u = (uint32_t)h16[k] << 16;
-          std::memcpy(&host_[k], &u, 4);
-        } else {
-          _Float16 hh;
-          std::memcpy(&hh, &h16[k], 2);
-          host_[k] = (float)hh;
-        }
-      }
-      NTXENT_HIP_CHECK(hipMemcpy(b_.h, h16.data(), R * dim * 2, hipMemcpyHostToDevice));
-    }
-    NTXENT_HIP_CHECK(hipStreamCreate(&s_));
-    ws_.num_cus = ncus;
-    ws_.bytes = gemm_workspace_bytes(std::max(b_.n_fwd, b_.n_dz), ncus);
-    NTXENT_HIP_CHECK(hipMalloc(&ws_.ptr, ws_.bytes));
+  Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed)
+      : in_(in) {
+    EngineConfig c;
+    c.rows = 2 * batch;
+    c.dim = dim;
+    c.temperature = T;
+    c.input = in;
+    c.compute = comp;
+    c.keep_cos = keep_cos;
+    host_ = synthetic_views(c.rows, dim, seed);
+    h_ = upload(host_, in);
+    NTXENT_HIP_CHECK(hipMalloc(&dh_, host_.size() * dtype_size(in)));
+    NTXENT_HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
+    e_ = std::make_unique<Engine>(c, comm);
   }
   ~Bench() {
-    hipFree(b_.h); hipFree(b_.dh); hipFree(b_.zq); hipFree(b_.zqt); hipFree(b_.inv); hipFree(b_.ypos);
-    hipFree(b_.part); hipFree(b_.sbuf); hipFree(b_.cbuf); hipFree(b_.lse2); hipFree(b_.cpos);
-    hipFree(b_.block_loss); hipFree(b_.loss); hipFree(b_.grad_out); hipFree(b_.slabs);
-    hipFree(b_.fwd_tiles); hipFree(b_.dz_tiles); hipFree(ws_.ptr);
+    e_.reset();
+    hipFree(h_);
+    hipFree(dh_);
     hipStreamDestroy(s_);
   }
 
-  void fwd() {
-    launch_prep(in_, comp_, b_.h, b_.zq, b_.inv, b_.ypos, g_, s_);
-    launch_transpose(comp_, b_.zq, b_.zqt, g_, s_);
-    launch_fwd_stats(comp_, b_.zq, b_.zq, b_.fwd_tiles, b_.n_fwd, b_.part, b_.sbuf, ws_, g_, s_);
-    launch_lse(b_.part, b_.ypos, b_.lse2, b_.cpos, b_.block_loss, b_.loss, g_, s_);
-  }
-  void bwd() {
-    launch_coef(comp_, b_.sbuf, b_.cbuf, b_.lse2, b_.cpos, b_.fwd_tiles, b_.n_fwd, g_, s_);
-    launch_dz(comp_, b_.cbuf, b_.zqt, b_.dz_tiles, b_.n_dz, b_.slabs, ws_, g_, s_);
-    launch_norm_bwd(in_, b_.slabs, b_.ksplit, b_.h, b_.inv, b_.grad_out, b_.dh, g_, s_);
-  }
+  void fwd() { e_->forward(h_, s_); }
+  void bwd() { e_->backward(nullptr, dh_, s_); }
 
-  // times `which` (0 fwd, 1 bwd, 2 fwd+bwd) with hipEvents; returns per-run ms
+  // times `which` (0 fwd, 1 bwd, 2 fwd+bwd, 3 fwd+bwd as one hipGraph) with hipEvents
   std::vector<float> time(int which, int warmup, int iters) {
     hipEvent_t a, b;
     NTXENT_HIP_CHECK(hipEventCreate(&a));
     NTXENT_HIP_CHECK(hipEventCreate(&b));
+    if (which == 3 && !e_->captured()) e_->capture(h_, dh_, s_);
     auto run = [&]() {
       if (which == 0) fwd();
       else if (which == 1) bwd();
-      else { fwd(); bwd(); }
+      else if (which == 2) { fwd(); bwd(); }
+      else e_->replay(s_);
     };
     if (which == 1) fwd();
     for (int i = 0; i < warmup; ++i) run();
@@ -191,16 +158,12 @@ class Bench {
     return out;
   }
 
-  float loss() {
-    float l = 0;
-    NTXENT_HIP_CHECK(hipStreamSynchronize(s_));
-    NTXENT_HIP_CHECK(hipMemcpy(&l, b_.loss, 4, hipMemcpyDeviceToHost));
-    return l;
-  }
+  float loss() { return e_->loss(s_); }
 
-  // host fp64 NT-Xent of the same inputs (small shapes only)
+  // host fp64 NT-Xent of the same inputs (small shapes, world 1 only)
   double host_loss() const {
-    const int R = g_.rows, d = g_.dim, n = R / 2;
+    const Geometry& g = e_->geometry();
+    const int R = g.rows, d = g.dim, n = R / 2;
     std::vector<double> z((size_t)R * d);
     for (int i = 0; i < R; ++i) {
       double ss = 0;
@@ -215,7 +178,7 @@ class Bench {
       for (int j = 0; j < R; ++j) {
         double s = 0;
         for (int e = 0; e < d; ++e) s += z[(size_t)i * d + e] * z[(size_t)j * d + e];
-        row[j] = s / g_.temperature;
+        row[j] = s / g.temperature;
         if (j != i) mx = std::max(mx, row[j]);
       }
       double se = 0;
@@ -226,16 +189,16 @@ class Bench {
     return tot / R;
   }
 
-  const Geometry& geom() const { return g_; }
-  int n_fwd() const { return b_.n_fwd; }
+  const Geometry& geom() const { return e_->geometry(); }
+  const Engine& engine() const { return *e_; }
 
  private:
-  DType in_, comp_;
-  Geometry g_;
-  Buffers b_;
-  GemmWorkspace ws_;
-  hipStream_t s_ = nullptr;
+  DType in_;
   std::vector<float> host_;
+  void* h_ = nullptr;
+  void* dh_ = nullptr;
+  hipStream_t s_ = nullptr;
+  std::unique_ptr<Engine> e_;
 };
 
 DType parse_dtype(const std::string& s) {
@@ -244,33 +207,102 @@ DType parse_dtype(const std::string& s) {
   return DType::BF16;
 }
 
-double fwd_flops(const Geometry& g) {
-  const double R = g.rows, d = g.dim;
-  return R * R * d;  // upper-triangular S (2 R^2 d / 2)
+// Useful MFMA FLOPs of one rank's fwd+bwd: upper-triangular own block + remote blocks (fwd),
+// full dZ GEMM over all global columns (bwd).
+double step_flops(const Geometry& g) {
+  const double R = g.rows, d = g.dim, RG = (double)g.global_rows;
+  return R * R * d + 2.0 * R * (RG - R) * d + 2.0 * R * RG * d;
 }
-double bwd_flops(const Geometry& g) { return 2.0 * g.rows * (double)g.rows * g.dim; }
+
+struct Options {
+  int batch = 0, dim = 0, iters = 100, warmup = 1, gpus = 1;
+  std::string dtype = "bf16", compute = "auto", json;
+  float T = 0.07f;
+  bool check = false, graph = false, recompute = false;
+};
+
+// Minimal reusable thread barrier (C++17).
+class ThreadBarrier {
+ public:
+  explicit ThreadBarrier(int n) : n_(n) {}
+  void wait() {
+    std::unique_lock<std::mutex> l(m_);
+    const int gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(l, [&] { return gen != gen_; });
+    }
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, gen_ = 0;
+};
+
+// Data-parallel run: one thread per GPU, one RCCL communicator per thread (no MPI needed);
+// every rank holds `batch` pairs, negatives are global. Reports the slowest rank.
+int run_multi(const Options& o, DType in, DType comp) {
+  const int N = o.gpus;
+  const std::string uid = RcclComm::unique_id();
+  ThreadBarrier bar(N);
+  std::vector<double> mean_ms(N, 0.0);
+  std::vector<std::string> errs(N);
+  double flops = 0;
+  float loss = 0;
+  std::vector<std::thread> th;
+  for (int r = 0; r < N; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        NTXENT_HIP_CHECK(hipSetDevice(r));
+        RcclComm comm(r, N, uid, r);
+        Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, &comm, 1234 + r);
+        bar.wait();
+        const Result fb = stats(bench.time(o.graph ? 3 : 2, o.warmup, o.iters));
+        mean_ms[r] = fb.mean;
+        if (r == 0) { flops = step_flops(bench.geom()); loss = bench.loss(); }
+        bar.wait();
+      } catch (const std::exception& e) {
+        errs[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int r = 0; r < N; ++r)
+    if (!errs[r].empty()) { std::fprintf(stderr, "rank %d: %s\n", r, errs[r].c_str()); return 1; }
+  const double ms = *std::max_element(mean_ms.begin(), mean_ms.end());
+  std::printf("gpus=%d B/gpu=%d D=%d %s: fwd+bwd %.4f ms (slowest rank), %.1f samples/s total, "
+              "%.1f TFLOP/s/GPU, loss %.6f\n", N, o.batch, o.dim, o.dtype.c_str(), ms,
+              (double)N * o.batch / (ms * 1e-3), flops / (ms * 1e-3) / 1e12, loss);
+  return 0;
+}
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  int batch = 0, dim = 0, iters = 100, warmup = 1;
-  std::string dtype = "bf16", compute = "auto";
-  float T = 0.07f;
-  bool check = false;
+  Options o;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() { return std::string(i + 1 < argc ? argv[++i] : ""); };
-    if (a == "--batch") batch = std::stoi(next());
-    else if (a == "--dim") dim = std::stoi(next());
-    else if (a == "--iters") iters = std::stoi(next());
-    else if (a == "--warmup") warmup = std::stoi(next());
-    else if (a == "--dtype") dtype = next();
-    else if (a == "--compute") compute = next();
-    else if (a == "--temperature") T = std::stof(next());
-    else if (a == "--check") check = true;
+    if (a == "--batch") o.batch = std::stoi(next());
+    else if (a == "--dim") o.dim = std::stoi(next());
+    else if (a == "--iters") o.iters = std::stoi(next());
+    else if (a == "--warmup") o.warmup = std::stoi(next());
+    else if (a == "--dtype") o.dtype = next();
+    else if (a == "--compute") o.compute = next();
+    else if (a == "--temperature") o.T = std::stof(next());
+    else if (a == "--gpus") o.gpus = std::stoi(next());
+    else if (a == "--json") o.json = next();
+    else if (a == "--check") o.check = true;
+    else if (a == "--graph") o.graph = true;
+    else if (a == "--recompute") o.recompute = true;
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32]\n"
-                  "                    [--iters N] [--warmup W] [--temperature T] [--check]\n");
+                  "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
+                  "                    [--recompute] [--gpus N] [--json out.json]\n");
       return 0;
     }
   }
@@ -279,29 +311,48 @@ int main(int argc, char** argv) {
   const DeviceInfo& di = device_info(dev);
   std::printf("Device: %s, %d CUs, matrix cores: %s\n", di.arch.c_str(), di.num_cus,
               check_matrix_core_support(dev) ? "yes (gfx950 MFMA)" : "no");
-  const DType in = parse_dtype(dtype);
-  const DType comp = compute == "auto" ? (in == DType::F32 ? DType::F32 : DType::F16) : parse_dtype(compute);
+  const DType in = parse_dtype(o.dtype);
+  const DType comp = o.compute == "auto" ? (in == DType::F32 ? DType::F32 : DType::F16) : parse_dtype(o.compute);
+  if (o.gpus > 1) {
+    if (o.batch <= 0) o.batch = 4096;
+    if (o.dim <= 0) o.dim = 2048;
+    return run_multi(o, in, comp);
+  }
 
   std::vector<std::pair<int, int>> shapes;
-  if (batch > 0) {
-    shapes.push_back({batch, dim > 0 ? dim : 2048});
+  if (o.batch > 0) {
+    shapes.push_back({o.batch, o.dim > 0 ? o.dim : 2048});
   } else {  // the reference sweep (src/benchmark.cpp:68-71)
     for (int b : {32, 64, 128, 256, 512, 1024})
       for (int d : {64, 128, 256}) shapes.push_back({b, d});
   }
-  std::printf("%6s %6s %5s | %-38s | %-38s | %-38s | %12s %9s\n", "B", "D", "dtype",
+  std::printf("%6s %6s %5s | %-38s | %-38s | %-38s | %-10s | %12s %9s\n", "B", "D", "dtype",
               "fwd ms: mean / std / min / max", "bwd ms: mean / std / min / max",
-              "fwd+bwd ms: mean / std / min / max", "samples/s", "TFLOP/s");
+              "fwd+bwd ms: mean / std / min / max", "graph ms", "samples/s", "TFLOP/s");
+  FILE* jf = o.json.empty() ? nullptr : std::fopen(o.json.c_str(), "w");
+  if (jf) std::fprintf(jf, "{\"device\": \"%s\", \"results\": {", di.arch.c_str());
+  bool first = true;
   for (auto [b, d] : shapes) {
-    Bench bench(b, d, in, comp, T, di.num_cus);
-    const Result f = stats(bench.time(0, warmup, iters));
-    const Result bw = stats(bench.time(1, warmup, iters));
-    const Result fb = stats(bench.time(2, warmup, iters));
-    const double tf = (fwd_flops(bench.geom()) + bwd_flops(bench.geom())) / (fb.mean * 1e-3) / 1e12;
-    std::printf("%6d %6d %5s | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %12.1f %9.1f\n",
-                b, d, dtype.c_str(), f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn, bw.mx, fb.mean,
-                fb.stdev, fb.mn, fb.mx, b / (fb.mean * 1e-3), tf);
-    if (check && b <= 1024 && d <= 512) {
+    Bench bench(b, d, in, comp, o.T, !o.recompute, nullptr, 1234);
+    const Result f = stats(bench.time(0, o.warmup, o.iters));
+    const Result bw = stats(bench.time(1, o.warmup, o.iters));
+    const Result fb = stats(bench.time(2, o.warmup, o.iters));
+    const Result gr = o.graph ? stats(bench.time(3, o.warmup, o.iters)) : Result{};
+    const double best = o.graph ? std::min(gr.mean, fb.mean) : fb.mean;
+    const double tf = step_flops(bench.geom()) / (best * 1e-3) / 1e12;
+    std::printf("%6d %6d %5s | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %10.4f | %12.1f %9.1f\n",
+                b, d, o.dtype.c_str(), f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn, bw.mx, fb.mean,
+                fb.stdev, fb.mn, fb.mx, gr.mean, b / (best * 1e-3), tf);
+    if (jf) {
+      std::fprintf(jf, "%s\n  \"B=%d,d=%d,dtype=%s,world=1\": {\"fwd_ms\": [%.5f, %.5f, %.5f, %.5f], "
+                   "\"bwd_ms\": [%.5f, %.5f, %.5f, %.5f], \"fwd_bwd_ms\": [%.5f, %.5f, %.5f, %.5f], "
+                   "\"graph_ms\": %.5f, \"samples_per_s\": %.1f, \"tflops\": %.2f, \"device_bytes\": %zu}",
+                   first ? "" : ",", b, d, o.dtype.c_str(), f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn,
+                   bw.mx, fb.mean, fb.stdev, fb.mn, fb.mx, gr.mean, b / (best * 1e-3), tf,
+                   bench.engine().device_bytes());
+      first = false;
+    }
+    if (o.check && b <= 1024 && d <= 512) {
       bench.fwd();
       const double ref = bench.host_loss();
       const double got = bench.loss();
@@ -311,6 +362,10 @@ int main(int argc, char** argv) {
         return 1;
       }
     }
+  }
+  if (jf) {
+    std::fprintf(jf, "\n}}\n");
+    std::fclose(jf);
   }
   return 0;
 }

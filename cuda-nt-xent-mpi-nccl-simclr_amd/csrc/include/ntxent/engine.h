@@ -1,0 +1,109 @@
+// ntxent-mi355x — native (libtorch-free) NT-Xent runtime.
+//
+// The reference's C++ surface is a pair of ATen functions that allocate O((2N)^2) buffers per
+// call (src/ntxent_kernel.cu:138-239). Engine is the MI355X-native replacement for C++
+// users, the native benchmark and the C++ tests:
+//
+//   * one arena allocation per (shape, dtype, world) sized up front — no allocation, host
+//     sync or host decision inside a step, so a whole fwd+bwd step is hipGraph-capturable
+//     (capture()/replay()) and replays with no per-kernel launch overhead;
+//   * data parallel through a Comm (RCCL over xGMI): prep writes this rank's normalised rows
+//     straight into its slot of the gathered buffer, the all-gathers run on a high-priority
+//     comm stream while the own-rank (upper-triangular) tiles are computed, and only the
+//     remote tiles wait for them; the ZqT gather is waited for only by the backward;
+//   * roctx ranges per stage (NTXENT_ROCTX=1) and fault-injection sites (NTXENT_FAULT).
+//
+// Usage:
+//   ntxent::Engine e({/*rows=*/8192, /*dim=*/2048, 0.07f, DType::BF16, DType::F16});
+//   e.forward(h, stream); e.backward(nullptr, dh, stream);  float l = e.loss(stream);
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "ntxent/comm.h"
+#include "ntxent/ntxent.h"
+
+namespace ntxent {
+
+struct EngineConfig {
+  int rows = 0;               // local rows R = 2 x per-view batch ([view1; view2] stacked)
+  int dim = 0;
+  float temperature = 0.07f;
+  DType input = DType::BF16;  // dtype of h / dh
+  DType compute = DType::F16; // MFMA operand dtype (fp32 = exact path)
+  bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
+  bool check_finite = false;  // loss() throws on a non-finite loss
+  int device = -1;            // -1: current device
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg, Comm* comm = nullptr);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  // Asynchronous on `stream`. h: device [rows][dim] (input dtype). The loss lands in
+  // loss_device() (global mean over all ranks).
+  void forward(const void* h, hipStream_t stream);
+  // grad_out: device fp32 scalar, or nullptr for 1. dh: device [rows][dim] (input dtype).
+  // Requires the preceding forward() of the same h.
+  void backward(const float* grad_out, void* dh, hipStream_t stream);
+  void step(const void* h, void* dh, hipStream_t stream) {
+    forward(h, stream);
+    backward(nullptr, dh, stream);
+  }
+
+  // hipGraph of one step() for fixed h / dh pointers; replay() launches it.
+  void capture(const void* h, void* dh, hipStream_t stream);
+  void replay(hipStream_t stream);
+  bool captured() const { return exec_ != nullptr; }
+
+  float loss(hipStream_t stream);  // synchronises `stream`
+  const float* loss_device() const { return loss_; }
+  const float* lse2_device() const { return lse2_all_; }  // [W*Rpad], log2 units
+  const float* inv_norm_device() const { return inv_; }
+  const Geometry& geometry() const { return g_; }
+  const EngineConfig& config() const { return cfg_; }
+  size_t device_bytes() const { return arena_bytes_; }
+  int fwd_tiles() const { return n_fwd_; }
+  int own_tiles() const { return n_own_; }
+  int dz_tiles() const { return n_dz_; }
+  Comm* comm() const { return comm_; }
+
+ private:
+  EngineConfig cfg_;
+  Geometry g_;
+  Comm* comm_ = nullptr;
+  const void* h_ = nullptr;  // input of the last forward (read by the backward)
+  int rank_ = 0, world_ = 1, device_ = 0;
+  int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
+  size_t cs_ = 2;
+  void* arena_ = nullptr;
+  size_t arena_bytes_ = 0;
+  char* zq_all_ = nullptr;
+  char* zqt_all_ = nullptr;
+  float* inv_ = nullptr;
+  float* ypos_ = nullptr;
+  float2* part_ = nullptr;
+  char* sbuf_ = nullptr;
+  char* cbuf_ = nullptr;
+  float* lse2_all_ = nullptr;
+  float* cpos_ = nullptr;
+  float* block_loss_ = nullptr;
+  float* loss_ = nullptr;
+  float* one_ = nullptr;
+  float* slabs_ = nullptr;
+  int4* fwd_tiles_ = nullptr;
+  int4* dz_tiles_ = nullptr;
+  GemmWorkspace ws_;
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t ev_prep_ = nullptr, ev_zq_ = nullptr, ev_zqt_ = nullptr;
+  bool zqt_pending_ = false;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+}  // namespace ntxent

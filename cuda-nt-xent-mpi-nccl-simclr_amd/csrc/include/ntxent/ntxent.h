@@ -93,8 +93,10 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
 // Tile kinds of the forward / coefficient pass.
 enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2 };
 
-// Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only.
+// Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
+// first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered.
 std::vector<int4> build_fwd_tiles(const Geometry& g);
+int count_own_fwd_tiles(const Geometry& g);
 // dZ tiles (ti, tn, ks, 0) for a split-K factor.
 std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit);
 // Split-K factor for the dZ GEMM; the stream-K schedule balances K itself, so this is 1.

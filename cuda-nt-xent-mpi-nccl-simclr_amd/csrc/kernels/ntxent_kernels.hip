@@ -372,23 +372,21 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
 }
 
 std::vector<int4> build_fwd_tiles(const Geometry& g) {
-  // Order: panel-major so that a run of consecutive tiles (one XCD's share after the
+  // Own-rank block first (upper triangle: S is symmetric), then the remote column blocks.
+  // Within each part panel-major, so a run of consecutive tiles (one XCD's share after the
   // xcd_remap) shares its A row panel and walks neighbouring B panels.
   std::vector<int4> tiles;
   const int own = g.rank * g.row_tiles;
-  for (int ti = 0; ti < g.row_tiles; ++ti) {
-    for (int tj = 0; tj < g.col_tiles; ++tj) {
-      const int local = tj - own;
-      if (local >= 0 && local < g.row_tiles) {
-        if (local < ti) continue;  // lower triangle: mirrored from (local, ti)
-        tiles.push_back(make_int4(ti, tj, local == ti ? kTileDiag : kTileSymOff, 0));
-      } else {
-        tiles.push_back(make_int4(ti, tj, kTilePlain, 0));
-      }
-    }
-  }
+  for (int ti = 0; ti < g.row_tiles; ++ti)
+    for (int local = ti; local < g.row_tiles; ++local)
+      tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
+  for (int ti = 0; ti < g.row_tiles; ++ti)
+    for (int tj = 0; tj < g.col_tiles; ++tj)
+      if (tj < own || tj >= own + g.row_tiles) tiles.push_back(make_int4(ti, tj, kTilePlain, 0));
   return tiles;
 }
+
+int count_own_fwd_tiles(const Geometry& g) { return g.row_tiles * (g.row_tiles + 1) / 2; }
 
 int choose_dz_ksplit(const Geometry& g, int num_cus) {
   // The persistent stream-K schedule of every similarity GEMM balances K itself, so the dZ

@@ -1,0 +1,203 @@
+// Native NT-Xent runtime (see include/ntxent/engine.h).
+//
+// Replaces the reference host launchers ntxent_forward_cuda / ntxent_backward_cuda
+// (src/ntxent_kernel.cu:138-203, 205-239): those allocate the 2N x 2N logits, softmax and
+// grad_logits per call and run cuBLAS on the legacy stream; here every buffer lives in one
+// arena sized once, all work is stream-ordered (graph-capturable) and collectives overlap
+// the own-rank tiles.
+#include "ntxent/engine.h"
+
+#include <cmath>
+#include <stdexcept>
+#include <vector>
+
+#include "ntxent/trace.h"
+
+namespace ntxent {
+namespace {
+
+constexpr size_t kAlign = 256;
+
+size_t align_up(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+}  // namespace
+
+Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
+  NTXENT_TRACE("ntxent.engine.init");
+  if (cfg.device >= 0) NTXENT_HIP_CHECK(hipSetDevice(cfg.device));
+  NTXENT_HIP_CHECK(hipGetDevice(&device_));
+  rank_ = comm ? comm->rank() : 0;
+  world_ = comm ? comm->world() : 1;
+  g_ = make_geometry(cfg.rows, cfg.dim, world_, rank_, cfg.temperature);
+  cs_ = dtype_size(cfg.compute);
+
+  const auto ft = build_fwd_tiles(g_);
+  const auto dt = build_dz_tiles(g_, 1);
+  n_fwd_ = (int)ft.size();
+  n_own_ = count_own_fwd_tiles(g_);
+  n_dz_ = (int)dt.size();
+  ws_.num_cus = device_info(device_).num_cus;
+  ws_.bytes = gemm_workspace_bytes(std::max(n_fwd_, n_dz_), ws_.num_cus);
+
+  const size_t W = world_, Rp = g_.rows_pad, R = g_.rows;
+  struct Slot { void** p; size_t bytes; };
+  const std::vector<Slot> slots = {
+      {(void**)&zq_all_, W * Rp * g_.ld_k * cs_},
+      {(void**)&zqt_all_, W * g_.dim_n * g_.ld_t * cs_},
+      {(void**)&inv_, R * 4},
+      {(void**)&ypos_, R * 4},
+      {(void**)&part_, (size_t)g_.col_tiles * Rp * sizeof(float2)},
+      {(void**)&sbuf_, cfg.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
+      {(void**)&cbuf_, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
+      {(void**)&lse2_all_, W * Rp * 4},
+      {(void**)&cpos_, Rp * 4},
+      {(void**)&block_loss_, (Rp / kTile) * 4 + 64},
+      {(void**)&loss_, 4},
+      {(void**)&one_, 4},
+      {(void**)&slabs_, Rp * g_.dim_n * 4},
+      {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
+      {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
+      {&ws_.ptr, ws_.bytes},
+  };
+  size_t total = 0;
+  for (const auto& s : slots) total += align_up(s.bytes);
+  arena_bytes_ = total;
+  NTXENT_HIP_CHECK(hipMalloc(&arena_, total));
+  char* base = static_cast<char*>(arena_);
+  for (const auto& s : slots) {
+    *s.p = s.bytes ? base : nullptr;
+    base += align_up(s.bytes);
+  }
+  NTXENT_HIP_CHECK(hipMemcpy(fwd_tiles_, ft.data(), ft.size() * sizeof(int4), hipMemcpyHostToDevice));
+  NTXENT_HIP_CHECK(hipMemcpy(dz_tiles_, dt.data(), dt.size() * sizeof(int4), hipMemcpyHostToDevice));
+  const float one = 1.0f;
+  NTXENT_HIP_CHECK(hipMemcpy(one_, &one, 4, hipMemcpyHostToDevice));
+  if (world_ > 1) {
+    int lo = 0, hi = 0;
+    NTXENT_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    NTXENT_HIP_CHECK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
+    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev_prep_, hipEventDisableTiming));
+    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev_zq_, hipEventDisableTiming));
+    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev_zqt_, hipEventDisableTiming));
+  }
+}
+
+Engine::~Engine() {
+  if (exec_) hipGraphExecDestroy(exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  if (ev_prep_) hipEventDestroy(ev_prep_);
+  if (ev_zq_) hipEventDestroy(ev_zq_);
+  if (ev_zqt_) hipEventDestroy(ev_zqt_);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+  if (arena_) hipFree(arena_);
+}
+
+void Engine::forward(const void* h, hipStream_t s) {
+  NTXENT_TRACE("ntxent.forward");
+  h_ = h;
+  const size_t Rp = g_.rows_pad;
+  char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
+  char* zqt_local = zqt_all_ + (size_t)rank_ * g_.dim_n * g_.ld_t * cs_;
+  {
+    NTXENT_TRACE("ntxent.prep");
+    fault_point("prep");
+    launch_prep(cfg_.input, cfg_.compute, h, zq_local, inv_, ypos_, g_, s);
+    launch_transpose(cfg_.compute, zq_local, zqt_local, g_, s);
+  }
+  if (world_ > 1) {
+    // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
+    NTXENT_HIP_CHECK(hipEventRecord(ev_prep_, s));
+    NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_prep_, 0));
+    comm_->all_gather(zq_local, zq_all_, Rp * g_.ld_k * cs_, comm_stream_);
+    NTXENT_HIP_CHECK(hipEventRecord(ev_zq_, comm_stream_));
+    comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
+    NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
+    zqt_pending_ = true;
+  }
+  {
+    NTXENT_TRACE("ntxent.fwd_gemm.own");
+    fault_point("fwd");
+    launch_fwd_stats(cfg_.compute, zq_local, zq_all_, fwd_tiles_, n_own_, part_, sbuf_, ws_, g_, s);
+  }
+  if (n_fwd_ > n_own_) {
+    NTXENT_TRACE("ntxent.fwd_gemm.remote");
+    if (world_ > 1) NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zq_, 0));
+    launch_fwd_stats(cfg_.compute, zq_local, zq_all_, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
+                     sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_, g_, s);
+  }
+  {
+    NTXENT_TRACE("ntxent.lse");
+    fault_point("lse");
+    launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
+  }
+  if (world_ > 1) {
+    NTXENT_TRACE("ntxent.lse_gather");
+    comm_->all_gather(lse2_all_ + (size_t)rank_ * Rp, lse2_all_, Rp * 4, s);
+    comm_->all_reduce_sum(loss_, 1, s);
+  }
+  if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
+}
+
+void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
+  NTXENT_TRACE("ntxent.backward");
+  NTXENT_CHECK(h_ != nullptr, "backward() before forward()");
+  const size_t Rp = g_.rows_pad;
+  const char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
+  {
+    NTXENT_TRACE("ntxent.coef");
+    fault_point("coef");
+    if (cfg_.keep_cos)
+      launch_coef(cfg_.compute, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s);
+    else
+      launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s);
+  }
+  if (zqt_pending_) {
+    NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));
+    zqt_pending_ = false;
+  }
+  {
+    NTXENT_TRACE("ntxent.dz_gemm");
+    fault_point("dz");
+    launch_dz(cfg_.compute, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s);
+  }
+  {
+    NTXENT_TRACE("ntxent.norm_bwd");
+    fault_point("norm_bwd");
+    launch_norm_bwd(cfg_.input, slabs_, 1, h_, inv_, grad_out ? grad_out : one_, dh, g_, s);
+  }
+}
+
+void Engine::capture(const void* h, void* dh, hipStream_t s) {
+  NTXENT_TRACE("ntxent.graph.capture");
+  fault_point("graph");
+  NTXENT_CHECK(s != nullptr, "graph capture needs a non-default stream");
+  if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
+  if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+  NTXENT_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  try {
+    step(h, dh, s);
+  } catch (...) {
+    hipGraph_t g = nullptr;
+    hipStreamEndCapture(s, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  NTXENT_HIP_CHECK(hipStreamEndCapture(s, &graph_));
+  NTXENT_HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+}
+
+void Engine::replay(hipStream_t s) {
+  NTXENT_CHECK(exec_ != nullptr, "replay() before capture()");
+  NTXENT_HIP_CHECK(hipGraphLaunch(exec_, s));
+}
+
+float Engine::loss(hipStream_t s) {
+  float l = 0.f;
+  NTXENT_HIP_CHECK(hipMemcpyAsync(&l, loss_, 4, hipMemcpyDeviceToHost, s));
+  NTXENT_HIP_CHECK(hipStreamSynchronize(s));
+  if (comm_) comm_->check();
+  if (cfg_.check_finite && !std::isfinite(l)) throw std::runtime_error("ntxent: non-finite loss");
+  return l;
+}
+
+}  // namespace ntxent

@@ -55,6 +55,7 @@ struct Plan {
   int device = 0;
   at::Tensor fwd_tiles;  // int32 [n, 4] on device
   int n_fwd = 0;
+  int n_own = 0;  // own-rank tiles at the head of fwd_tiles
   at::Tensor dz_tiles;
   int n_dz = 0;
   int ksplit = 1;
@@ -98,6 +99,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->num_cus = di.num_cus;
   auto ft = build_fwd_tiles(p->g);
   p->n_fwd = (int)ft.size();
+  p->n_own = count_own_fwd_tiles(p->g);
   p->fwd_tiles = upload_tiles(ft, device);
   p->ksplit = choose_dz_ksplit(p->g, di.num_cus);
   auto dt = build_dz_tiles(p->g, p->ksplit);
@@ -132,11 +134,21 @@ static std::pair<at::Tensor, GemmWorkspace> gemm_ws(const at::Tensor& like, int 
 }
 
 // ---- stage ops ----------------------------------------------------------------------
-std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
+// `zq_out` (optional): write the normalised rows into this [rows_pad, ld_k] buffer — e.g. this
+// rank's slot of the all-gather destination, so the gather runs in place.
+std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::optional<at::Tensor>& zq_out) {
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
   const at::DeviceGuard guard(h.device());
-  auto zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.comp)));
+  at::Tensor zq;
+  if (zq_out.has_value() && zq_out->defined()) {
+    zq = *zq_out;
+    check_input(zq, "zq_out");
+    NTXENT_CHECK(zq.numel() == (long)P.g.rows_pad * P.g.ld_k && zq.scalar_type() == to_scalar(P.comp),
+                 "zq_out must be [rows_pad, ld_k] in the compute dtype");
+  } else {
+    zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.comp)));
+  }
   auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
   auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
   launch_prep(to_dtype(h.scalar_type()), P.comp, h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(),
@@ -144,10 +156,18 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P) {
   return {zq, inv, ypos};
 }
 
-at::Tensor transpose(const at::Tensor& zq, const Plan& P) {
+at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at::Tensor>& zqt_out) {
   check_input(zq, "zq");
   const at::DeviceGuard guard(zq.device());
-  auto zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
+  at::Tensor zqt;
+  if (zqt_out.has_value() && zqt_out->defined()) {
+    zqt = *zqt_out;
+    check_input(zqt, "zqt_out");
+    NTXENT_CHECK(zqt.numel() == (long)P.g.dim_n * P.g.ld_t && zqt.scalar_type() == zq.scalar_type(),
+                 "zqt_out must be [dim_n, ld_t]");
+  } else {
+    zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
+  }
   launch_transpose(P.comp, zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
 }
@@ -168,6 +188,29 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
                    reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
                    ws.second, P.g, cur_stream(zq_local));
   return {part, sc};
+}
+
+// Forward tiles [first, first + count) of the plan's list into caller-owned `part` / `sc`
+// (sc may be undefined). The own-rank tiles come first (P.n_own of them) and read only this
+// rank's slot of zq_all, so they can run while the rest of zq_all is being gathered.
+void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P, at::Tensor& part,
+                     const c10::optional<at::Tensor>& sc, int first, int count) {
+  check_input(zq_local, "zq_local");
+  check_input(zq_all, "zq_all");
+  check_input(part, "part");
+  NTXENT_CHECK(first >= 0 && count >= 0 && first + count <= P.n_fwd, "tile range out of bounds");
+  NTXENT_CHECK(part.numel() == (long)P.g.col_tiles * P.g.rows_pad * 2 && part.scalar_type() == at::kFloat,
+               "part must be float32 [col_tiles, rows_pad, 2]");
+  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.g.ld_k, "zq_all must be [world*rows_pad, ld_k]");
+  const bool keep = sc.has_value() && sc->defined();
+  if (keep) NTXENT_CHECK(sc->numel() == (long)P.n_fwd * kTileElems, "sc must hold n_fwd tiles");
+  if (count == 0) return;
+  const at::DeviceGuard guard(zq_local.device());
+  auto ws = gemm_ws(zq_local, count, P);
+  char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.comp) : nullptr;
+  launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
+                   reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws.second, P.g, cur_stream(zq_local));
 }
 
 // Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
@@ -240,10 +283,12 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2, "z must be 2-D [2N, d]");
   const at::DeviceGuard guard(h.device());
-  const DType comp = choose_compute(h.scalar_type(), compute != "fp32", compute);
+  // "auto" = the input-dtype policy (fp32 stays exact); mixed precision is requested by the
+  // callers as an explicit "fp16".
+  const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
-  auto pr = prep(h, *P);
-  auto zqt = transpose(pr[0], *P);
+  auto pr = prep(h, *P, c10::nullopt);
+  auto zqt = transpose(pr[0], *P, c10::nullopt);
   auto fs = fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
@@ -292,8 +337,8 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   const at::DeviceGuard guard(z.device());
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
-  auto pr = prep(z, *P);
-  auto zqt = transpose(pr[0], *P);
+  auto pr = prep(z, *P, c10::nullopt);
+  auto zqt = transpose(pr[0], *P, c10::nullopt);
   auto lse2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
   auto fs = fwd_stats(pr[0], pr[0], *P, false);
@@ -372,6 +417,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("temperature", &Plan::temperature)
       .def_property_readonly("compute_dtype", &Plan::compute_dtype)
       .def_readonly("n_fwd_tiles", &Plan::n_fwd)
+      .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("ksplit", &Plan::ksplit)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
@@ -382,8 +428,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::ScalarType t = in_dtype == "float32" ? at::kFloat : (in_dtype == "float16" ? at::kHalf : at::kBFloat16);
     return std::string(ntxent::dtype_name(choose_compute(t, mp, ov)));
   });
-  m.def("prep", &prep);
-  m.def("transpose", &transpose);
+  m.def("prep", &prep, py::arg("h"), py::arg("plan"), py::arg("zq_out") = py::none());
+  m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
+  m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
+        py::arg("sc"), py::arg("first"), py::arg("count"));
   m.def("fwd_stats", &fwd_stats);
   m.def("lse", &lse);
   m.def("coef", &coef);

@@ -1,0 +1,110 @@
+// RCCL implementation of ntxent::Comm (see include/ntxent/comm.h).
+#include "ntxent/comm.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "ntxent/ntxent.h"
+#include "ntxent/trace.h"
+
+#define NTXENT_RCCL_CHECK(expr)                                                               \
+  do {                                                                                        \
+    ncclResult_t _r = (expr);                                                                 \
+    if (_r != ncclSuccess) {                                                                  \
+      throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + " in " #expr);     \
+    }                                                                                         \
+  } while (0)
+
+namespace ntxent {
+
+static_assert(sizeof(ncclUniqueId) == RcclComm::kIdBytes, "ncclUniqueId size");
+
+void LocalComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
+  if (send != recv && bytes) NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream));
+}
+
+std::string RcclComm::unique_id() {
+  ncclUniqueId id;
+  NTXENT_RCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+std::string RcclComm::version() {
+  int v = 0;
+  NTXENT_RCCL_CHECK(ncclGetVersion(&v));
+  return std::to_string(v);
+}
+
+RcclComm::RcclComm(int rank, int world, const std::string& id, int device, AllGatherAlgo algo)
+    : rank_(rank), world_(world), algo_(algo) {
+  NTXENT_CHECK(world >= 1 && rank >= 0 && rank < world, "RcclComm: bad rank/world");
+  NTXENT_CHECK(id.size() == kIdBytes, "RcclComm: unique id must be 128 bytes");
+  if (device >= 0) NTXENT_HIP_CHECK(hipSetDevice(device));
+  NTXENT_HIP_CHECK(hipGetDevice(&device_));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id.data(), sizeof(uid));
+  ncclComm_t c = nullptr;
+  NTXENT_TRACE("ntxent.rccl.init");
+  NTXENT_RCCL_CHECK(ncclCommInitRank(&c, world, uid, rank));
+  comm_ = c;
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ && !aborted_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
+  NTXENT_TRACE("ntxent.allgather");
+  fault_point("allgather");
+  NTXENT_CHECK(!aborted_, "RcclComm: communicator aborted");
+  auto c = static_cast<ncclComm_t>(comm_);
+  if (world_ == 1) {
+    if (send != recv) NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream));
+    return;
+  }
+  if (algo_ == AllGatherAlgo::kRccl) {
+    NTXENT_RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclChar, c, stream));
+    return;
+  }
+  // Mesh: own shard to every peer and every peer's shard straight into its slot, all in one
+  // group so the 7 xGMI links run concurrently (a ring would use one link per step).
+  char* out = static_cast<char*>(recv);
+  char* own = out + (size_t)rank_ * bytes;
+  if (send != own) NTXENT_HIP_CHECK(hipMemcpyAsync(own, send, bytes, hipMemcpyDeviceToDevice, stream));
+  NTXENT_RCCL_CHECK(ncclGroupStart());
+  for (int k = 1; k < world_; ++k) {
+    const int to = (rank_ + k) % world_, from = (rank_ - k + world_) % world_;
+    NTXENT_RCCL_CHECK(ncclSend(own, bytes, ncclChar, to, c, stream));
+    NTXENT_RCCL_CHECK(ncclRecv(out + (size_t)from * bytes, bytes, ncclChar, from, c, stream));
+  }
+  NTXENT_RCCL_CHECK(ncclGroupEnd());
+}
+
+void RcclComm::all_reduce_sum(float* buf, size_t count, hipStream_t stream) {
+  NTXENT_TRACE("ntxent.allreduce");
+  fault_point("allreduce");
+  NTXENT_CHECK(!aborted_, "RcclComm: communicator aborted");
+  if (world_ == 1) return;
+  NTXENT_RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+}
+
+void RcclComm::check() {
+  if (!comm_ || aborted_) return;
+  ncclResult_t async = ncclSuccess;
+  NTXENT_RCCL_CHECK(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &async));
+  if (async != ncclSuccess && async != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL async error: ") + ncclGetErrorString(async));
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(static_cast<ncclComm_t>(comm_));
+    aborted_ = true;
+  }
+}
+
+}  // namespace ntxent

@@ -42,19 +42,29 @@ class DistNTXentFunction(torch.autograd.Function):
         h = h.contiguous()
         R, d = h.shape
         plan = C.get_plan(R, d, W, r, float(temperature), compute, h.device.index)
-        zq, inv, ypos = C.prep(h, plan)
         Rpad = plan.rows_pad
-        zq_all = torch.empty((W * Rpad, plan.ld_k), dtype=zq.dtype, device=h.device)
-        zqt = C.transpose(zq, plan)
-        zqt_all = torch.empty((W, plan.dim_n, plan.ld_t), dtype=zq.dtype, device=h.device)
+        cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[plan.compute_dtype]
+        # prep / transpose write straight into this rank's slot: the gathers run in place.
+        zq_all = torch.empty((W * Rpad, plan.ld_k), dtype=cdt, device=h.device)
+        zqt_all = torch.empty((W, plan.dim_n, plan.ld_t), dtype=cdt, device=h.device)
+        zq = zq_all[r * Rpad:(r + 1) * Rpad]
+        zqt = zqt_all[r]
+        _, inv, ypos = C.prep(h, plan, zq)
+        C.transpose(zq, plan, zqt)
+        work_z = work_t = None
         if W > 1:
-            work_z = dist.all_gather_into_tensor(zq_all, zq, group=group, async_op=overlap)
+            work_z = dist.all_gather_into_tensor(zq_all, zq, group=group, async_op=True)
             work_t = dist.all_gather_into_tensor(zqt_all, zqt, group=group, async_op=True)
-            if overlap:
+            if not overlap:
                 work_z.wait()
-        else:
-            zq_all, zqt_all, work_t = zq, zqt.unsqueeze(0), None
-        part, sc = C.fwd_stats(zq, zq_all, plan, bool(keep_logits))
+                work_z = None
+        part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=h.device)
+        sc = torch.empty((plan.n_fwd_tiles * 256 * 256,), dtype=cdt, device=h.device) if keep_logits else None
+        # own-rank (upper-triangular) tiles need only this rank's slot: they overlap the gather
+        C.fwd_stats_range(zq, zq_all, plan, part, sc, 0, plan.n_own_tiles)
+        if work_z is not None:
+            work_z.wait()
+        C.fwd_stats_range(zq, zq_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles)
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)

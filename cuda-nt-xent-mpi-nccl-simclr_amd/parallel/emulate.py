@@ -1,0 +1,64 @@
+"""Single-GPU emulation of the W-rank data-parallel NT-Xent (testing / debugging aid).
+
+Runs every virtual rank's stage ops (the same HIP kernels and per-rank plans the RCCL path
+uses: own-rank upper-triangular tiles, remote column blocks with global column indices,
+per-rank LSE slot, rank-local symmetric backward) sequentially on one device. The
+collectives are replaced by construction: each rank's ``prep``/``transpose`` writes into its
+slot of the shared gathered buffers, and each rank's LSE lands in its slot of ``lse2_all``.
+This is what lets a 1-GPU box verify the multi-GPU math bit-for-bit (the real path differs
+only in who fills the other slots).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+from ..ops import _ext
+from ..ops.ntxent import resolve_compute
+
+
+def emulated_dist_forward_backward(shards: Sequence[torch.Tensor], temperature: float, *, compute: str = "auto",
+                                   keep_logits: bool = True, grad_out: float = 1.0
+                                   ) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """Loss (global mean over all W*R rows) and per-rank dL/dh_r for shards h_r = [h1_r; h2_r]."""
+    C = _ext.load()
+    W = len(shards)
+    R, d = shards[0].shape
+    dev = shards[0].device
+    comp = resolve_compute(shards[0].dtype, False, compute)
+    plans = [C.get_plan(R, d, W, r, float(temperature), comp, dev.index) for r in range(W)]
+    P0 = plans[0]
+    Rpad = P0.rows_pad
+    cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[P0.compute_dtype]
+    zq_all = torch.empty((W * Rpad, P0.ld_k), dtype=cdt, device=dev)
+    zqt_all = torch.empty((W, P0.dim_n, P0.ld_t), dtype=cdt, device=dev)
+    invs, yposs = [], []
+    for r in range(W):  # "all-gather" of Zq / ZqT: every rank writes its own slot
+        zq = zq_all[r * Rpad:(r + 1) * Rpad]
+        _, inv, ypos = C.prep(shards[r].contiguous(), plans[r], zq)
+        C.transpose(zq, plans[r], zqt_all[r])
+        invs.append(inv)
+        yposs.append(ypos)
+    lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=dev)
+    loss = torch.zeros((), dtype=torch.float32, device=dev)
+    scs, cposs = [], []
+    for r in range(W):
+        P = plans[r]
+        part = torch.empty((P.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
+        sc = torch.empty((P.n_fwd_tiles * 256 * 256,), dtype=cdt, device=dev) if keep_logits else None
+        zq = zq_all[r * Rpad:(r + 1) * Rpad]
+        C.fwd_stats_range(zq, zq_all, P, part, sc, 0, P.n_fwd_tiles)
+        cpos = torch.empty((Rpad,), dtype=torch.float32, device=dev)
+        loss = loss + C.lse(part, yposs[r], lse2_all, cpos, P)  # "all-gather" of LSE + "all-reduce"
+        scs.append(sc)
+        cposs.append(cpos)
+    go = torch.tensor([grad_out], dtype=torch.float32, device=dev)
+    grads = []
+    for r in range(W):
+        P = plans[r]
+        zq = zq_all[r * Rpad:(r + 1) * Rpad]
+        cb = C.coef(scs[r], lse2_all, cposs[r], P) if keep_logits else C.coef_gemm(zq, zq_all, lse2_all, cposs[r], P)
+        slabs = C.dz(cb, zqt_all, P)
+        grads.append(C.norm_bwd(slabs, shards[r].contiguous(), invs[r], go, P))
+    return loss, grads

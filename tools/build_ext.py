@@ -29,6 +29,22 @@ ARCH = os.environ.get("NTXENT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+RUNTIME_SRCS = ["engine.cpp", "rccl_comm.cpp", "trace.cpp"]
+
+
+def _host_cxx():
+    """hipcc as a plain host C++ compiler (no device pass) for runtime / torch / tool TUs."""
+    return [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-std=c++17", "-fPIC", "-I/opt/rocm/include"]
+
+
+def _feature_defines():
+    """Compile-time feature switches (mirrors the CMake options)."""
+    d = []
+    if os.environ.get("NTXENT_ENABLE_PROFILING", "0") == "1":
+        d.append("-DNTXENT_PROFILING_DEFAULT=1")
+    return d
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension as ce
@@ -95,24 +111,33 @@ def build(force: bool = False, cpp_targets: bool = True, verbose: bool = False) 
             "-Wno-deprecated-declarations",
         ]
         # host-only translation unit: compile as plain C++ (no device pass over libtorch headers)
-        hostc = [HIPCC, "-x", "c++", "-D__HIP_PLATFORM_AMD__=1", "-std=c++17", "-fPIC", "-I/opt/rocm/include", f"-I{CSRC / 'include'}"]
+        hostc = _host_cxx() + [f"-I{CSRC / 'include'}"]
         jobs.append(hostc + tflags + ["-c", str(t_src), "-o", str(t_obj)])
-    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+    # native runtime (engine, RCCL communicator, tracing): host-only C++ against the HIP runtime
+    rt_objs = []
+    for name in RUNTIME_SRCS:
+        src = CSRC / "runtime" / name
+        obj = BUILD / (Path(name).stem + ".o")
+        rt_objs.append(obj)
+        if force or _stale(obj, [src, *hdrs]):
+            jobs.append(_host_cxx() + [f"-I{CSRC / 'include'}", "-O2", *_feature_defines(), "-c", str(src), "-o", str(obj)])
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs))
 
     so = ext_path()
-    if force or _stale(so, [k_obj, t_obj]):
-        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(k_obj), str(t_obj), "-o", str(so),
-                f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-                f"-Wl,-rpath,{tlib}"]
+    if force or _stale(so, [k_obj, t_obj, *rt_objs]):
+        # RCCL: bind to the copy torch ships (one RCCL instance per process)
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(k_obj), str(t_obj), *map(str, rt_objs),
+                "-o", str(so), f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+                "-ltorch_python", "-lrccl", "-ldl", f"-Wl,-rpath,{tlib}"]
         _run(link, verbose)
 
     if cpp_targets:
-        build_cpp_targets(k_obj, force=force, verbose=verbose)
+        build_cpp_targets([k_obj, *rt_objs], force=force, verbose=verbose)
     return so
 
 
-def build_cpp_targets(k_obj: Path, force: bool = False, verbose: bool = False):
+def build_cpp_targets(objs, force: bool = False, verbose: bool = False):
     """Standalone C++ executables (no libtorch): benchmark + tests over the raw API."""
     hdrs = _headers()
     targets = {
@@ -122,10 +147,11 @@ def build_cpp_targets(k_obj: Path, force: bool = False, verbose: bool = False):
     def one(name, src):
         out = BUILD / "bin" / name
         obj = BUILD / f"{name}.o"
-        if force or _stale(out, [src, k_obj, *hdrs]):
-            _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O2", f"-I{CSRC / 'include'}", "-c", str(src),
-                  "-o", str(obj)], verbose)
-            _run([HIPCC, f"--offload-arch={ARCH}", str(obj), str(k_obj), "-o", str(out)], verbose)
+        if force or _stale(out, [src, *objs, *hdrs]):
+            _run(_host_cxx() + [f"-I{CSRC / 'include'}", "-O2", *_feature_defines(), "-c", str(src), "-o", str(obj)],
+                 verbose)
+            _run([HIPCC, f"--offload-arch={ARCH}", str(obj), *map(str, objs), "-o", str(out), "-L/opt/rocm/lib",
+                  "-lrccl", "-ldl", "-Wl,-rpath,/opt/rocm/lib"], verbose)
 
     with cf.ThreadPoolExecutor(max_workers=2) as ex:
         list(ex.map(lambda kv: one(*kv), [(n, s) for n, s in targets.items() if s.exists()]))
