@@ -36,11 +36,51 @@ uint16_t f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// IEEE binary16 conversions in plain C++ (round to nearest even; host compilers without
+// _Float16 build this too).
 uint16_t f32_to_f16(float f) {
-  _Float16 h = (_Float16)f;
-  uint16_t u;
-  std::memcpy(&u, &h, 2);
-  return u;
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const int32_t exp = (int32_t)((x >> 23) & 0xFF) - 127 + 15;
+  uint32_t man = x & 0x7FFFFFu;
+  if (((x >> 23) & 0xFF) == 0xFF) return (uint16_t)(sign | 0x7C00u | (man ? 0x200u : 0u));  // inf / nan
+  if (exp >= 31) return (uint16_t)(sign | 0x7C00u);                                          // overflow
+  if (exp <= 0) {                                                                            // subnormal / zero
+    if (exp < -10) return (uint16_t)sign;
+    man |= 0x800000u;
+    const int shift = 14 - exp;
+    uint32_t h = man >> shift;
+    const uint32_t rem = man & ((1u << shift) - 1), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((uint32_t)exp << 10) | (man >> 13);
+  const uint32_t rem = man & 0x1FFFu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;  // may carry into the exponent: correct
+  return (uint16_t)(sign | h);
+}
+
+float f16_to_f32(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+  uint32_t exp = (h >> 10) & 0x1Fu, man = h & 0x3FFu, x;
+  if (exp == 0) {
+    if (man == 0) {
+      x = sign;
+    } else {  // normalise the subnormal
+      exp = 1;
+      while (!(man & 0x400u)) { man <<= 1; --exp; }
+      man &= 0x3FFu;
+      x = sign | ((exp + 127 - 15) << 23) | (man << 13);
+    }
+  } else if (exp == 31) {
+    x = sign | 0x7F800000u | (man << 13);
+  } else {
+    x = sign | ((exp + 127 - 15) << 23) | (man << 13);
+  }
+  float f;
+  std::memcpy(&f, &x, 4);
+  return f;
 }
 
 struct Result {
@@ -92,9 +132,7 @@ void* upload(std::vector<float>& host, DType in) {
       uint32_t u = (uint32_t)h16[k] << 16;
       std::memcpy(&host[k], &u, 4);
     } else {
-      _Float16 hh;
-      std::memcpy(&hh, &h16[k], 2);
-      host[k] = (float)hh;
+      host[k] = f16_to_f32(h16[k]);
     }
   }
   NTXENT_HIP_CHECK(hipMemcpy(d, h16.data(), n * 2, hipMemcpyHostToDevice));

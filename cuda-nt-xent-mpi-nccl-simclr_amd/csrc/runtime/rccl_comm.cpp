@@ -1,14 +1,35 @@
 // RCCL implementation of ntxent::Comm (see include/ntxent/comm.h).
 #include "ntxent/comm.h"
 
-#include <rccl/rccl.h>
-
 #include <cstring>
 #include <stdexcept>
 #include <string>
 
 #include "ntxent/ntxent.h"
 #include "ntxent/trace.h"
+
+namespace ntxent {
+void LocalComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
+  if (send != recv && bytes) NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream));
+}
+}  // namespace ntxent
+
+#ifdef NTXENT_NO_RCCL
+namespace ntxent {
+namespace {
+[[noreturn]] void no_rccl() { throw std::runtime_error("ntxent: built without RCCL (ENABLE_RCCL=OFF)"); }
+}  // namespace
+std::string RcclComm::unique_id() { no_rccl(); }
+std::string RcclComm::version() { return "none"; }
+RcclComm::RcclComm(int, int, const std::string&, int, AllGatherAlgo algo) : algo_(algo) { no_rccl(); }
+RcclComm::~RcclComm() = default;
+void RcclComm::all_gather(const void*, void*, size_t, hipStream_t) { no_rccl(); }
+void RcclComm::all_reduce_sum(float*, size_t, hipStream_t) { no_rccl(); }
+void RcclComm::check() {}
+void RcclComm::abort() {}
+}  // namespace ntxent
+#else
+#include <rccl/rccl.h>
 
 #define NTXENT_RCCL_CHECK(expr)                                                               \
   do {                                                                                        \
@@ -22,10 +43,6 @@
 namespace ntxent {
 
 static_assert(sizeof(ncclUniqueId) == RcclComm::kIdBytes, "ncclUniqueId size");
-
-void LocalComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
-  if (send != recv && bytes) NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream));
-}
 
 std::string RcclComm::unique_id() {
   ncclUniqueId id;
@@ -108,3 +125,4 @@ void RcclComm::abort() {
 }
 
 }  // namespace ntxent
+#endif  // NTXENT_NO_RCCL
