@@ -371,18 +371,38 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
   return g;
 }
 
+// Morton (Z-order) key: every aligned run of 2^k consecutive tiles is a compact 2-D block.
+static unsigned morton2(unsigned i, unsigned j) {
+  unsigned r = 0;
+  for (int b = 0; b < 16; ++b) r |= ((i >> b) & 1u) << (2 * b + 1) | ((j >> b) & 1u) << (2 * b);
+  return r;
+}
+
+static void zorder(std::vector<int4>& t, size_t first, size_t last) {
+  std::stable_sort(t.begin() + first, t.begin() + last, [](const int4& a, const int4& b) {
+    return morton2((unsigned)a.x, (unsigned)a.y) < morton2((unsigned)b.x, (unsigned)b.y);
+  });
+}
+
 std::vector<int4> build_fwd_tiles(const Geometry& g) {
   // Own-rank block first (upper triangle: S is symmetric), then the remote column blocks.
-  // Within each part panel-major, so a run of consecutive tiles (one XCD's share after the
-  // xcd_remap) shares its A row panel and walks neighbouring B panels.
+  // Each part in Z-order: the blocks of one XCD (consecutive logical ids after xcd_remap) take
+  // consecutive tiles, and a Z-order run of 32 tiles touches ~0.4 distinct row panels per tile
+  // (A and B panels of the own block are both rows of Zq) versus ~0.7-1.0 for panel-major
+  // order, which is what the forward GEMM's L2 hit rate depends on (measured 48% before).
   std::vector<int4> tiles;
   const int own = g.rank * g.row_tiles;
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int local = ti; local < g.row_tiles; ++local)
       tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
+  const size_t n_own = tiles.size();
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int tj = 0; tj < g.col_tiles; ++tj)
       if (tj < own || tj >= own + g.row_tiles) tiles.push_back(make_int4(ti, tj, kTilePlain, 0));
+  if (std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1) {
+    zorder(tiles, 0, n_own);
+    zorder(tiles, n_own, tiles.size());
+  }
   return tiles;
 }
 
