@@ -114,6 +114,8 @@ struct GemmSchedule {
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus);
 
 // Scratch of one similarity-GEMM launch: arrival counters + 2 fp32 partial tiles per block.
+// Must be ZERO when first used; every launch leaves the counters zero again, so one
+// workspace serves any number of stream-ordered launches (no per-launch memset).
 struct GemmWorkspace {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -145,7 +147,10 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
 // -(sigmoid(lse_neg_i - y) + sigmoid(lse_neg_p - y)) (well conditioned when P_ip -> 1).
 // loss_sum[0] receives sum_i softplus(lse_neg_i - y_i) / (W*R) over this rank's rows
-// (all-reduce SUM across ranks gives the loss). `block_loss` is scratch of Rpad/256 floats.
+// (all-reduce SUM across ranks gives the loss). `block_loss` is scratch of
+// lse_scratch_floats(g) floats that must be ZERO when first used (the kernel leaves it
+// reusable: its arrival counter returns to zero).
+int lse_scratch_floats(const Geometry& g);
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos,
                 float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream);
 

@@ -139,15 +139,9 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
   }
 }
 
-// Row statistics of one row from its negatives-only partials: returns lse2 and writes the
-// natural-log loss term softplus(lse_neg - y_pos) and a = 1 - P_ip = sigmoid(lse_neg - y_pos).
-__device__ __forceinline__ float row_stats(const float2* __restrict__ part, int i, int Rpad, int Tc, float yp,
-                                           float& loss, float& a) {
-  float m = kNegInf, s = 0.f;
-  for (int t = 0; t < Tc; ++t) {
-    const float2 v = part[(long long)t * Rpad + i];
-    lse_merge(m, s, v.x, v.y);
-  }
+// Row statistics from a row's merged negatives-only (max, sum) state: returns lse2 and writes
+// the natural-log loss term softplus(lse_neg - y_pos) and a = 1 - P_ip = sigmoid(lse_neg - y_pos).
+__device__ __forceinline__ float finish_row(float m, float s, float yp, float& loss, float& a) {
   const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
   const float mx = fmaxf(neg2, yp);  // lse = logaddexp(lse_neg, y_pos)
   const float l2 = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
@@ -157,41 +151,72 @@ __device__ __forceinline__ float row_stats(const float2* __restrict__ part, int 
   return l2;
 }
 
-// One thread per positive pair (i, i+n) (plus the pad rows): LSE of both rows, their loss
-// terms, and the positive coefficient C_ip = P_ip + P_pi - 2 = -(a_i + a_p), formed without
-// the 1 - P cancellation.
+// Eight lanes per positive pair (i, i+n): lane q merges column tiles q, q+8, ... of both rows,
+// an xor-shuffle tree merges the eight states, lane 0 finishes: LSE of both rows, their loss
+// terms and the positive coefficient C_ip = P_ip + P_pi - 2 = -(a_i + a_p) (no 1 - P
+// cancellation). Pad rows [R, Rpad) get zeros. One thread per pair left the chip ~94% idle
+// (16 workgroups for B = 4096) and serialised 32-64 dependent merges per thread.
+constexpr int kLseLanes = 8;
 __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ part, const float* __restrict__ ypos,
                                                   float* __restrict__ lse2_all, float* __restrict__ cpos,
-                                                  float* __restrict__ block_loss, int R, int Rpad, int Tc, int own0) {
+                                                  float* __restrict__ block_loss, float* __restrict__ loss_sum,
+                                                  float loss_scale, int R, int Rpad, int Tc, int own0) {
   __shared__ float red[16];
   const int n = R >> 1;
-  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int gt = blockIdx.x * 256 + threadIdx.x;
+  const int item = gt / kLseLanes, q = gt % kLseLanes;
   float li = 0.f;
-  if (t < n) {
-    const int i = t, j = t + n;
-    const float yp = ypos[i];
-    float l_i, l_j, a_i, a_j;
-    const float l2i = row_stats(part, i, Rpad, Tc, yp, l_i, a_i);
-    const float l2j = row_stats(part, j, Rpad, Tc, yp, l_j, a_j);
-    lse2_all[own0 + i] = l2i;
-    lse2_all[own0 + j] = l2j;
-    cpos[i] = -(a_i + a_j);
-    cpos[j] = -(a_i + a_j);
-    li = l_i + l_j;
-  } else if (t < Rpad - n) {
-    const int i = R + (t - n);
+  if (item < n) {  // uniform across the 8 lanes of an item
+    const int i = item, j = item + n;
+    float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
+    for (int t = q; t < Tc; t += kLseLanes) {
+      const float2 vi = part[(long long)t * Rpad + i];
+      const float2 vj = part[(long long)t * Rpad + j];
+      lse_merge(mi, si, vi.x, vi.y);
+      lse_merge(mj, sj, vj.x, vj.y);
+    }
+#pragma unroll
+    for (int off = 1; off < kLseLanes; off <<= 1) {
+      lse_merge(mi, si, __shfl_xor(mi, off), __shfl_xor(si, off));
+      lse_merge(mj, sj, __shfl_xor(mj, off), __shfl_xor(sj, off));
+    }
+    if (q == 0) {
+      const float yp = ypos[i];
+      float l_i, l_j, a_i, a_j;
+      lse2_all[own0 + i] = finish_row(mi, si, yp, l_i, a_i);
+      lse2_all[own0 + j] = finish_row(mj, sj, yp, l_j, a_j);
+      cpos[i] = -(a_i + a_j);
+      cpos[j] = -(a_i + a_j);
+      li = l_i + l_j;
+    }
+  } else if (item < Rpad - n && q == 0) {
+    const int i = R + (item - n);
     lse2_all[own0 + i] = 0.f;
     cpos[i] = 0.f;
   }
   const float tot = block_sum(li, red);
-  if (threadIdx.x == 0) block_loss[blockIdx.x] = tot;
-}
-
-__global__ void loss_final_kernel(const float* __restrict__ block_loss, int nb, float scale, float* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  // Last-block-done final sum (replaces a separate one-thread launch): publish this block's
+  // partial, count arrivals; the last block adds all partials in block order (deterministic)
+  // and returns the counter (a fixed slot ahead of the partials) to zero.
+  __shared__ int last;
+  int* cnt = reinterpret_cast<int*>(block_loss);  // fixed slot 0: the counter
+  float* partial = block_loss + 64;               // per-block partials after it
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = tot;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == (int)gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (last && threadIdx.x < 64) {
     float s = 0.f;
-    for (int b = 0; b < nb; ++b) s += block_loss[b];  // fixed order: deterministic
-    out[0] = s * scale;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += 64) s += partial[b];
+    s = wave_sum(s);  // fixed lane assignment and tree: deterministic
+    if (threadIdx.x == 0) loss_sum[0] = s * loss_scale;
   }
 }
 
@@ -305,8 +330,12 @@ dev::SimParams base_params(const Geometry& g) {
   return p;
 }
 
-// Fill the stream-K fields of `p` for `ntiles` tiles of p.kbytes each and zero the arrival
-// counters (a memset node, so the launch sequence stays graph-capturable). Returns the grid.
+// Fill the stream-K fields of `p` for `ntiles` tiles of p.kbytes each. The arrival counters at
+// the head of the workspace are zero when it is allocated and every launch leaves them zero
+// (the last arriver of a tile resets its counter), so no memset node is needed per launch.
+// Returns the grid.
+size_t sk_counter_bytes(int num_cus) { return ((size_t)2 * std::max(1, num_cus) * 4 + 255) / 256 * 256; }
+
 int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipStream_t stream) {
   NTXENT_CHECK(p.kbytes % kKStepBytes == 0, "K not aligned to the K step");
   const int nk = (int)(p.kbytes / kKStepBytes);
@@ -315,14 +344,15 @@ int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipSt
   p.dp_tiles = s.dp_tiles;
   p.sk_tiles = s.sk_tiles;
   p.ipb = s.ipb;
-  const size_t cnt_bytes = ((size_t)ntiles * 4 + 255) / 256 * 256;
+  const size_t cnt_bytes = sk_counter_bytes(ws.num_cus);  // fixed: independent of the launch
+  NTXENT_CHECK(s.sk_tiles <= 2 * ws.num_cus, "stream-K tile count exceeds the counter region");
   p.sk_cnt = static_cast<int*>(ws.ptr);
   p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + cnt_bytes);
-  if (s.sk_tiles > 0) {
+  if (s.sk_tiles > 0) {  // counters must be zero at launch: zeroed at allocation, self-cleaning
     NTXENT_CHECK(ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
                  "stream-K workspace too small");
-    NTXENT_HIP_CHECK(hipMemsetAsync(ws.ptr, 0, ((size_t)s.sk_tiles * 4 + 15) / 16 * 16, stream));
   }
+  (void)stream;
   return s.grid;
 }
 
@@ -437,9 +467,14 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   return s;
 }
 
+// Stream-K splits at most 2*G - 1 tiles (one DP round plus the remainder, or all tiles when
+// there are fewer than G), so 2*num_cus counters always suffice. The counter region has a
+// fixed size so that launches of different tile counts sharing one workspace never place
+// their fp32 partial slabs over another launch's (self-cleaning, zero) counters.
+
 size_t gemm_workspace_bytes(int ntiles, int num_cus) {
-  const size_t cnt = ((size_t)ntiles * 4 + 255) / 256 * 256;
-  return cnt + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float);
+  (void)ntiles;
+  return sk_counter_bytes(num_cus) + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float);
 }
 
 std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit) {
@@ -525,14 +560,15 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
+static int lse_blocks(const Geometry& g) { return ((g.rows_pad - g.rows / 2) * dev::kLseLanes + 255) / 256; }
+
+int lse_scratch_floats(const Geometry& g) { return 64 + lse_blocks(g); }  // counter slot + partials
+
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
                 float* loss_sum, const Geometry& g, hipStream_t stream) {
-  const int nb = (g.rows_pad - g.rows / 2 + 255) / 256;  // one thread per pair + pad rows
-  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, cpos, block_loss,
-                     g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad);
-  NTXENT_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(dev::loss_final_kernel, dim3(1), dim3(64), 0, stream, block_loss, nb,
-                     (float)(1.0 / (double)g.global_rows), loss_sum);
+  const int nb = lse_blocks(g);  // one workgroup per 32 pairs / pad rows
+  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, cpos, block_loss, loss_sum,
+                     (float)(1.0 / (double)g.global_rows), g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad);
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 

@@ -67,7 +67,7 @@ struct SimParams {
   int sk_tiles;          // tiles whose K-steps are split evenly over the grid
   long long ipb;         // stream-K K-steps per block
   float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
-  int* sk_cnt;           // [sk_tiles] arrival counters (zeroed before every launch)
+  int* sk_cnt;           // [sk_tiles] arrival counters (zero at launch; self-cleaning)
 };
 
 // Ablation bits (timing experiments only; results are garbage when set).
@@ -435,6 +435,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       if (last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // every contributor has arrived: return the counter to zero for the next launch
+        __hip_atomic_store(p.sk_cnt + stile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       flag[0] = last;
     }

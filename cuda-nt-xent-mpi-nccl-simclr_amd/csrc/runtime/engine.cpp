@@ -51,7 +51,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&cbuf_, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
       {(void**)&lse2_all_, W * Rp * 4},
       {(void**)&cpos_, Rp * 4},
-      {(void**)&block_loss_, (Rp / kTile) * 4 + 64},
+      {(void**)&block_loss_, (size_t)lse_scratch_floats(g_) * 4},
       {(void**)&loss_, 4},
       {(void**)&one_, 4},
       {(void**)&slabs_, Rp * g_.dim_n * 4},
@@ -68,6 +68,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     *s.p = s.bytes ? base : nullptr;
     base += align_up(s.bytes);
   }
+  // zero once: the stream-K and LSE arrival counters are self-cleaning afterwards
+  NTXENT_HIP_CHECK(hipMemset(arena_, 0, total));
   NTXENT_HIP_CHECK(hipMemcpy(fwd_tiles_, ft.data(), ft.size() * sizeof(int4), hipMemcpyHostToDevice));
   NTXENT_HIP_CHECK(hipMemcpy(dz_tiles_, dt.data(), dt.size() * sizeof(int4), hipMemcpyHostToDevice));
   const float one = 1.0f;

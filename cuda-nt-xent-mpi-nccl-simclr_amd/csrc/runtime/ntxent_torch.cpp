@@ -122,15 +122,27 @@ static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
   return at::TensorOptions().dtype(t).device(like.device());
 }
 
-// Stream-K scratch for one GEMM launch, from the caching allocator (released with the
-// returned tensor once the stream has consumed it).
-static std::pair<at::Tensor, GemmWorkspace> gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
+// Zero-initialised per-device scratch for the kernels' self-cleaning arrival counters
+// (stream-K tile arrivals, LSE last-block-done). Every launch returns its counters to zero, so
+// a buffer is zeroed only when it is (re)allocated, and no memset runs per launch. Launches
+// sharing a slot are stream-ordered (every op enqueues on the current stream; ops of one
+// device run on one stream in the autograd and data-parallel paths). A grown buffer replaces
+// the old one; the caching allocator keeps the old block alive until its stream is done.
+static at::Tensor device_scratch(const at::Tensor& like, size_t bytes, int slot) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, at::Tensor> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& t = cache[{(int)like.device().index(), slot}];
+  if (!t.defined() || (size_t)t.numel() < bytes) t = at::zeros({(long)bytes}, opts(like, at::kByte));
+  return t;
+}
+
+static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
   GemmWorkspace ws;
   ws.num_cus = P.num_cus;
   ws.bytes = gemm_workspace_bytes(ntiles, P.num_cus);
-  auto t = at::empty({(long)ws.bytes}, opts(like, at::kByte));
-  ws.ptr = t.data_ptr();
-  return {t, ws};
+  ws.ptr = device_scratch(like, ws.bytes, 0).data_ptr();
+  return ws;
 }
 
 // ---- stage ops ----------------------------------------------------------------------
@@ -186,7 +198,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
-                   ws.second, P.g, cur_stream(zq_local));
+                   ws, P.g, cur_stream(zq_local));
   return {part, sc};
 }
 
@@ -210,7 +222,7 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.comp) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
-                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws.second, P.g, cur_stream(zq_local));
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local));
 }
 
 // Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
@@ -222,10 +234,10 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
                "lse2_all must be float32 [world*rows_pad]");
   NTXENT_CHECK(cpos.numel() == P.g.rows_pad && cpos.scalar_type() == at::kFloat, "cpos must be float32 [rows_pad]");
   const at::DeviceGuard guard(part.device());
-  auto block_loss = at::empty({P.g.rows_pad / 256}, opts(part, at::kFloat));
+  auto block_loss = device_scratch(part, (size_t)lse_scratch_floats(P.g) * 4, 1);
   auto loss = at::empty({}, opts(part, at::kFloat));
   launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(),
-             lse2_all.data_ptr<float>(), cpos.data_ptr<float>(), block_loss.data_ptr<float>(),
+             lse2_all.data_ptr<float>(), cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()),
              loss.data_ptr<float>(), P.g, cur_stream(part));
   return loss;
 }
@@ -249,7 +261,7 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
-                   ws.second, P.g, cur_stream(zq_local));
+                   ws, P.g, cur_stream(zq_local));
   return cbuf;
 }
 
@@ -261,7 +273,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
   auto ws = gemm_ws(sc, P.n_dz, P);
   launch_dz(P.comp, sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
-            P.n_dz, slabs.data_ptr<float>(), ws.second, P.g, cur_stream(sc));
+            P.n_dz, slabs.data_ptr<float>(), ws, P.g, cur_stream(sc));
   return slabs;
 }
 
