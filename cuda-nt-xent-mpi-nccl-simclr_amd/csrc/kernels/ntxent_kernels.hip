@@ -17,8 +17,10 @@
 #include "sim_gemm.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 namespace ntxent {
@@ -312,6 +314,53 @@ void dispatch_comp(DType t, F&& f) {
   }
 }
 
+// Diagnostic builds (-DNTXENT_ABLATION_KERNELS) pick a compile-time ablation of the GEMM
+// main loop with NTXENT_GEMM_ABL=<bits>; production builds instantiate only ABL = 0.
+int gemm_ablation() {
+#ifdef NTXENT_ABLATION_KERNELS
+  static const int a = [] {
+    const char* e = std::getenv("NTXENT_GEMM_ABL");
+    return e ? std::atoi(e) : 0;
+  }();
+  return a;
+#else
+  return 0;
+#endif
+}
+
+template <typename Tc, int MODE>
+void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
+#ifdef NTXENT_ABLATION_KERNELS
+  if constexpr (std::is_same<Tc, _Float16>::value) switch (gemm_ablation()) {
+#define NTXENT_ABL_CASE(A) \
+    case A: hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); return;
+    NTXENT_ABL_CASE(1) NTXENT_ABL_CASE(2) NTXENT_ABL_CASE(3) NTXENT_ABL_CASE(4) NTXENT_ABL_CASE(5)
+    NTXENT_ABL_CASE(6) NTXENT_ABL_CASE(14) NTXENT_ABL_CASE(22) NTXENT_ABL_CASE(30)
+#undef NTXENT_ABL_CASE
+    case 32: {  // clock stamps of block 0 (waves 0 and 4), dumped to stderr (synchronising)
+      static unsigned long long* buf = nullptr;
+      if (!buf) NTXENT_HIP_CHECK(hipMalloc(&buf, 512 * 8));
+      NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, 512 * 8, stream));
+      dev::SimParams q = p;
+      q.stamps = buf;
+      hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 32>), dim3(grid), dim3(kGemmThreads), 0, stream, q);
+      unsigned long long h[512];
+      NTXENT_HIP_CHECK(hipMemcpyAsync(h, buf, sizeof(h), hipMemcpyDeviceToHost, stream));
+      NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
+      std::fprintf(stderr, "STAMPS mode=%d nk=%d", MODE, p.nk);
+      for (int g = 0; g < 2; ++g) {
+        std::fprintf(stderr, " | g%d:", g);
+        for (int i = 1; i < 256 && h[g * 256 + i]; ++i) std::fprintf(stderr, " %llu", h[g * 256 + i] - h[g * 256 + i - 1]);
+      }
+      std::fprintf(stderr, "\n");
+      return;
+    }
+    default: break;
+  }
+#endif
+  hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
+}
+
 dev::SimParams base_params(const Geometry& g) {
   dev::SimParams p{};
   p.R = g.rows;
@@ -531,8 +580,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeFwd>), dim3(grid), dim3(kGemmThreads), 0,
-                       stream, p);
+    launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }
@@ -554,8 +602,7 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeCoef>), dim3(grid), dim3(kGemmThreads), 0,
-                       stream, p);
+    launch_sim_gemm<Tc, dev::kModeCoef>(grid, p, stream);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }
@@ -614,8 +661,7 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, dev::kModeDz>), dim3(grid), dim3(kGemmThreads), 0,
-                       stream, p);
+    launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

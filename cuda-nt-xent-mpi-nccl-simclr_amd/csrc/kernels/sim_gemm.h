@@ -61,6 +61,7 @@ struct SimParams {
   long long ldo;         // elements
   long long slab_stride; // elements
   int dbg;               // diagnostic ablations (NTXENT_GEMM_DEBUG; 0 in production)
+  unsigned long long* stamps;  // ABL & 32 diagnostic builds: s_memtime per barrier
   // persistent stream-K schedule (see sim_gemm_kernel)
   int nk;                // K-steps per tile
   int dp_tiles;          // whole-tile items processed in rounds of gridDim
@@ -215,7 +216,10 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb
 // ------------------------------------------------------------------------------------
 // The similarity GEMM with its three epilogues (see the file header for the schedule).
 // ------------------------------------------------------------------------------------
-template <typename T, int MODE>
+// ABL: compile-time ablations for diagnostic builds only (production instantiates ABL = 0):
+// 1 = no global->LDS DMA, 2 = no LDS operand reads, 4 = no MFMA, 8 = deeper DMA queue,
+// 16 = no barriers (8 and 16 only make sense with 2|4), 32 = clock stamps (tools/ablate_ct.sh).
+template <typename T, int MODE, int ABL = 0>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
@@ -246,7 +250,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
     const char* src = (isB ? Bb : Ab) + s.kbo + s.kin;
-    if (!(p.dbg & kDbgNoLoads)) {
+    if (!(ABL & 1) && !(p.dbg & kDbgNoLoads)) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
@@ -260,6 +264,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
   frag af[2][4], bf0[2][2], bf1[2][2];  // [k-substep][block]
   auto read_a = [&](int buf, int h, frag (&af)[2][4]) {
+    if constexpr ((ABL & 2) != 0) {  // ablation: operands stay as they are, opaque to the compiler
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) asm volatile("" : "+v"(af[s][mi]));
+      return;
+    }
     const lds_char* As = lds + buf * kStageBytes;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -270,6 +281,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   };
   auto read_b = [&](int buf, int h, frag (&bf)[2][2]) {
+    if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) asm volatile("" : "+v"(bf[s][ni]));
+      return;
+    }
     const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -282,6 +300,16 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // s_setprio(1)/(0) around each MFMA cluster keeps hipcc from sinking the cluster across the
   // next s_barrier (cdna_hip_programming.md §5.5 T5).
   auto mma_quadrant = [&](int qa, int qb, frag (&af)[2][4], frag (&bf)[2][2]) {
+    if constexpr ((ABL & 4) != 0) {  // ablation: consume the operands, issue no MFMA
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) asm volatile("" ::"v"(af[s][mi]));
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) asm volatile("" ::"v"(bf[s][ni]));
+      }
+      return;
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -294,14 +322,25 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         }
     __builtin_amdgcn_s_setprio(0);
   };
+  int n_stamp = 0;  // ABL & 32: clock stamp after every barrier of K-steps [4, 12), block 0
+  const bool stamper = (ABL & 32) && bid == 0 && lane == 0 && (w == 0 || w == 4);
   auto barrier = [&]() {
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((ABL & 16) == 0) __builtin_amdgcn_s_barrier();  // ABL 16: no barriers (timing only)
     asm volatile("" ::: "memory");
+    if constexpr ((ABL & 32) != 0) {
+      if (stamper && n_stamp < 256) p.stamps[(w >> 2) * 256 + n_stamp] = __builtin_amdgcn_s_memtime();
+      ++n_stamp;
+    }
   };
   auto lds_drain = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  // phase 1 issues the 8 A0 reads before the 4 B0 reads; LDS reads retire in order
+  auto a0_retire = [&]() { asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); };
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
-  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  auto dma_wait = [&]() {
+    if constexpr ((ABL & 8) != 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // ABL 8: deeper queue (timing only)
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  };
   // Wave group (0: waves 0-3, 1: waves 4-7); each SIMD hosts one wave of each group.
   const int grp = __builtin_amdgcn_readfirstlane(w) >> 2;
 
@@ -310,14 +349,19 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // interval C (16 MFMA from registers), separated by barriers. Group 1 runs one barrier
   // behind group 0 (staggered ping-pong), so on every SIMD one wave's L overlaps its partner's
   // C and the MFMA pipe alternates between them (cdna_hip_programming.md §5, 8-phase).
-  //   phase 1: stage A1(t+1) | read A0(t) B0(t) | MFMA A0B0
-  //   phase 2: stage A0(t+2) | read B1(t)       | MFMA A0B1
-  //   phase 3: stage B0(t+2) | read A1(t)       | MFMA A1B0
-  //   phase 4: stage B1(t+2) |                  | MFMA A1B1
-  // Correctness under the stagger: a half-tile is re-staged one phase after its last read,
-  // and every read drains (lgkmcnt) before the next barrier, so the other group has finished
-  // reading it (WAR); DMA waits run one phase ahead, so both groups' copies of a half-tile
-  // retired before a barrier that precedes either group's read (RAW).
+  //   phase 1: read A0(t) B0(t) | stage A1(t+1) | MFMA A0B0
+  //   phase 2: read B1(t)       | stage A0(t+2) | MFMA A0B1
+  //   phase 3: read A1(t)       | stage B0(t+2) | MFMA A1B0
+  //   phase 4:                  | stage B1(t+2) | MFMA A1B1
+  // (reads are issued before the DMA pieces: a phase costs ~2 x max(L, C), and L is then
+  // the DMA issue time rather than DMA issue + read latency.)
+  // Correctness under the stagger. WAR: B0, B1 and A1 are re-staged two phases after their
+  // last read, and a read retires at the latest at the lgkmcnt(0) right after the next
+  // barrier, i.e. before the barrier that starts the re-staging phase of either group; A0 is
+  // re-staged ONE phase after its read, so its 8 reads (issued first) retire before the
+  // barrier ending their L interval (counted lgkmcnt(4)). RAW: DMA waits run one phase ahead,
+  // so both groups' copies of a half-tile retired before a barrier that precedes either
+  // group's read.
   //
   // Persistent stream-K schedule: the first dp_tiles tiles are whole-tile work items
   // (rounds of G); the remaining sk_tiles * nk K-steps are split evenly (ipb steps per block).
@@ -368,20 +412,22 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   for (int ks = 0; ks < nsteps; ++ks) {
     const int cur = ks & 1, nxt = cur ^ 1;
     dma_wait(); barrier();          // phase 1 L (wait covers B1(t) for phase 2)
+    read_a(cur, 0, af);             //   operand reads first: their latency hides under the
+    __builtin_amdgcn_sched_barrier(0);  // pin: the 8 A0 reads precede the B0 reads (a0_retire)
+    read_b(cur, 0, bf0);            //   DMA issue that follows (~100-200 cycles per piece)
     stage(0, 1, sa1, nxt);          //   A1 of step ks+1
-    read_a(cur, 0, af);
-    read_b(cur, 0, bf0);
-    lds_drain(); barrier();         // phase 1 C
+    a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
+    lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
     mma_quadrant(0, 0, af, bf0);
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
-    stage(0, 0, sa0, cur);          //   A0 of step ks+2
     read_b(cur, 1, bf1);
-    lds_drain(); barrier();         // phase 2 C
+    stage(0, 0, sa0, cur);          //   A0 of step ks+2
+    barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
     mma_quadrant(0, 1, af, bf1);
     barrier();                      // phase 3 L
-    stage(1, 0, sb0, cur);          //   B0 of step ks+2
     read_a(cur, 1, af);
-    lds_drain(); barrier();         // phase 3 C
+    stage(1, 0, sb0, cur);          //   B0 of step ks+2
+    barrier(); lds_drain();         // phase 3 C (A1 is restaged two phases later)
     mma_quadrant(1, 0, af, bf0);
     dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
