@@ -19,7 +19,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, dim, T, grad_out, q):
+def _worker(rank, world, port, n, dim, T, grad_out, q, mode="symmetric"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -28,18 +28,18 @@ def _worker(rank, world, port, n, dim, T, grad_out, q):
 
         g = torch.Generator().manual_seed(1000 + rank)
         h = torch.randn(2 * n, dim, generator=g, dtype=torch.float64).requires_grad_(True)
-        loss = dist_ntxent_loss(h, T)
+        loss = dist_ntxent_loss(h, T, backward_mode=mode)
         loss.backward(torch.tensor(grad_out, dtype=torch.float64))
         q.put((rank, loss.detach().numpy().copy(), h.detach().numpy().copy(), h.grad.detach().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, n, dim, T=0.1, grad_out=1.0):
+def _run(world, n, dim, T=0.1, grad_out=1.0, mode="symmetric"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, dim, T, grad_out, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, dim, T, grad_out, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     out = [q.get(timeout=120) for _ in range(world)]
@@ -49,12 +49,13 @@ def _run(world, n, dim, T=0.1, grad_out=1.0):
     return [(r, torch.from_numpy(l), torch.from_numpy(h), torch.from_numpy(g)) for r, l, h, g in sorted(out, key=lambda x: x[0])]
 
 
-@pytest.mark.parametrize("world,n,dim", [(2, 4, 8), (2, 5, 17), (3, 3, 6)])
-def test_gloo_matches_oracle(world, n, dim):
+@pytest.mark.parametrize("world,n,dim,mode", [(2, 4, 8, "symmetric"), (2, 5, 17, "symmetric"), (3, 3, 6, "symmetric"),
+                                              (2, 4, 8, "reduce_scatter"), (3, 3, 6, "reduce_scatter")])
+def test_gloo_matches_oracle(world, n, dim, mode):
     from ntxent_amd.ops import reference as ref
 
     T, go = 0.1, 0.7
-    res = _run(world, n, dim, T, go)
+    res = _run(world, n, dim, T, go, mode)
     shards = [r[2] for r in res]
     hg = ref.global_pair_order(shards).requires_grad_(True)
     l_ref = ref.ntxent_loss(hg, T)

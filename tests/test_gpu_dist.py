@@ -107,3 +107,16 @@ def test_rccl_path_world1(nccl_world1, overlap):
     (g2,) = torch.autograd.grad(l2, y)
     assert loss.item() == l2.item()
     assert torch.equal(g, g2)
+
+
+def test_rccl_reduce_scatter_backward_world1(nccl_world1):
+    import ntxent_amd
+    from ntxent_amd.parallel import dist_ntxent_loss
+
+    h = _shards(1, 256, 128, seed=9)[0].float().cuda()
+    x = h.clone().requires_grad_(True)
+    loss = dist_ntxent_loss(x, 0.1, compute="fp32", backward_mode="reduce_scatter")
+    (g,) = torch.autograd.grad(loss, x)
+    y = h.clone().requires_grad_(True)
+    (g2,) = torch.autograd.grad(ntxent_amd.ntxent_loss(y, 0.1, compute="fp32"), y)
+    torch.testing.assert_close(g, g2, rtol=1e-3, atol=1e-6)
