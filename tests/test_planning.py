@@ -90,5 +90,10 @@ def test_stream_k_schedule(C, ntiles, nk, cus):
 
 
 def test_workspace_bytes(C):
+    # fixed layout: 2*num_cus arrival counters (stream-K splits < 2G tiles) + 2 fp32 tiles per block,
+    # independent of the launch's tile count so launches can share one zero-initialised workspace
     b = C.gemm_workspace_bytes(528, 256)
-    assert b >= 528 * 4 + 2 * 256 * 256 * 256 * 4
+    assert b >= 2 * 256 * 4 + 2 * 256 * 256 * 256 * 4
+    assert b == C.gemm_workspace_bytes(7696, 256) == C.gemm_workspace_bytes(1, 256)
+    for nt, nk in [(528, 32), (7696, 32), (300, 7), (255, 3)]:
+        assert C.schedule(nt, nk, 256)["sk_tiles"] <= 2 * 256
