@@ -242,6 +242,7 @@ class Bench {
 DType parse_dtype(const std::string& s) {
   if (s == "fp32") return DType::F32;
   if (s == "fp16") return DType::F16;
+  if (s == "fp8") return DType::FP8;
   return DType::BF16;
 }
 
@@ -338,7 +339,7 @@ int main(int argc, char** argv) {
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
     else if (a == "-h" || a == "--help") {
-      std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32]\n"
+      std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
                   "                    [--recompute] [--gpus N] [--json out.json]\n");
       return 0;

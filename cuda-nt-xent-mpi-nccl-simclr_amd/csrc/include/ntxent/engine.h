@@ -32,7 +32,8 @@ struct EngineConfig {
   int dim = 0;
   float temperature = 0.07f;
   DType input = DType::BF16;  // dtype of h / dh
-  DType compute = DType::F16; // MFMA operand dtype (fp32 = exact path)
+  DType compute = DType::F16; // MFMA operand dtype (fp32 = exact path; FP8 = e4m3 forward GEMM,
+                              // fp16 backward, cosines always kept)
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
   bool check_finite = false;  // loss() throws on a non-finite loss
   int device = -1;            // -1: current device
@@ -80,10 +81,13 @@ class Engine {
   const void* h_ = nullptr;  // input of the last forward (read by the backward)
   int rank_ = 0, world_ = 1, device_ = 0;
   int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
-  size_t cs_ = 2;
+  size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
+  bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
+  DType bwd_ = DType::F16;
   void* arena_ = nullptr;
   size_t arena_bytes_ = 0;
   char* zq_all_ = nullptr;
+  char* zq8_all_ = nullptr;
   char* zqt_all_ = nullptr;
   float* inv_ = nullptr;
   float* ypos_ = nullptr;

@@ -46,12 +46,16 @@ constexpr int kGemmThreads = 512;   // 8 waves: 2 (M) x 4 (N), 128x64 per wave
 constexpr int kLdsPerCU = 160 * 1024;
 constexpr int kNumXcd = 8;
 
-enum class DType : int { F32 = 0, F16 = 1, BF16 = 2 };
+// FP8 (e4m3, OCP) is a forward-GEMM operand type only: an fp8 plan runs the similarity GEMM
+// on fp8 MFMA and keeps cosines / runs the backward in fp16.
+enum class DType : int { F32 = 0, F16 = 1, BF16 = 2, FP8 = 3 };
 
-inline size_t dtype_size(DType t) { return t == DType::F32 ? 4 : 2; }
+inline size_t dtype_size(DType t) { return t == DType::F32 ? 4 : (t == DType::FP8 ? 1 : 2); }
 inline const char* dtype_name(DType t) {
-  return t == DType::F32 ? "fp32" : (t == DType::F16 ? "fp16" : "bf16");
+  return t == DType::F32 ? "fp32" : (t == DType::F16 ? "fp16" : (t == DType::BF16 ? "bf16" : "fp8"));
 }
+// dtype of zq / ZqT / kept cosines / coefficients (the backward operands) for a plan dtype
+inline DType backward_dtype(DType t) { return t == DType::FP8 ? DType::F16 : t; }
 
 // Status-typed error check (the reference mis-types a cuBLAS status into AT_CUDA_CHECK at
 // src/ntxent_kernel.cu:166; here every HIP call goes through a hipError_t check).
@@ -79,6 +83,8 @@ struct Geometry {
   int dim_n = 0;       // roundup(d, 256): rows of ZqT (N of the dZ GEMM)
   int ld_k = 0;        // row stride (elements) of Zq: dim_k, de-aliased from powers of two
   int ld_t = 0;        // row stride (elements) of ZqT: rows_pad, de-aliased likewise
+  int dim_k8 = 0;      // roundup(d, 128): K bytes of an fp8 row (one 128-byte K-step = 128 elements)
+  int ld_k8 = 0;       // row stride (bytes) of the fp8 copy Zq8
   int world = 1;       // W ranks sharing negatives
   int rank = 0;
   int row_tiles = 0;   // Rpad / 256
@@ -129,8 +135,10 @@ size_t gemm_workspace_bytes(int ntiles, int num_cus);
 // Row L2-normalisation prologue: inv[i] = 1/max(||h_i||, 1e-12); zq = h*inv (compute
 // dtype, zero padded to dim_k); ypos[i] = <zq_i, zq_p(i)> * inv_temp * log2(e).
 // Pad rows [R, Rpad) of zq are zeroed.
+// zq8 (optional): also write the fp8 copy Zq8[Rpad][ld_k8] = e4m3(z * 256) for an fp8 forward;
+// ypos is then computed from the dequantised fp8 rows.
 void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
-                 const Geometry& g, hipStream_t stream);
+                 const Geometry& g, hipStream_t stream, void* zq8 = nullptr);
 
 // zqt[e][j] = zq[j][e] (zero for e >= dim_k). zqt is [dim_n][Rpad].
 void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g,

@@ -62,6 +62,33 @@ template <> struct Mfma<float> {
   }
 };
 
+// fp8 e4m3 (OCP, gfx950) operand type: the 128-byte K-step of a row holds 128 elements; a
+// 16-byte fragment feeds TWO v_mfma_f32_16x16x32_fp8_fp8 (its low and high 8 bytes). Lane l
+// of the fragment holds elements 16c..16c+15 of its chunk c, so each MFMA sums a fixed
+// permutation of 32 k positions — the same one for A and B, hence the exact dot product.
+struct fp8e4m3 {
+  unsigned char v;
+};
+template <> struct Mfma<fp8e4m3> {
+  typedef u32x4 frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    const long a0 = (long)a[0] | ((long)a[1] << 32), a1 = (long)a[2] | ((long)a[3] << 32);
+    const long b0 = (long)b[0] | ((long)b[1] << 32), b1 = (long)b[2] | ((long)b[3] << 32);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0, b0, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1, b1, c, 0, 0, 0);
+    return c;
+  }
+};
+
+// Element type used to store cosines / coefficients produced from a GEMM in operand type T
+// (fp8 GEMMs keep their outputs in fp16: the backward runs in fp16).
+template <typename T> struct StoreT { typedef T type; };
+template <> struct StoreT<fp8e4m3> { typedef _Float16 type; };
+
+// Per-tensor fp8 scale: normalised rows (|z| <= 1) are stored as e4m3(z * kFp8Scale); a power
+// of two, so scaling is exact and S = acc / kFp8Scale^2.
+constexpr float kFp8Scale = 256.0f;
+
 // ---- wave64 cross-lane reductions ----------------------------------------------------
 // DPP row_ror within a 16-lane row: 0x120 + n.
 template <int CTRL> __device__ __forceinline__ float dpp_f(float x) {

@@ -57,10 +57,32 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
   }
 }
 
-template <typename Tin, typename Tc>
+// fp8 e4m3 of 8 values (x * kFp8Scale), packed little-endian into 2 dwords; q receives the
+// dequantised values (what the fp8 GEMM multiplies), divided back by the scale.
+__device__ __forceinline__ u32x2 quant8(const float (&x)[8], float (&q)[8]) {
+  u32x2 r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int v = 0;
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * kFp8Scale, x[4 * h + 1] * kFp8Scale, v, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 2] * kFp8Scale, x[4 * h + 3] * kFp8Scale, v, true);
+    r[h] = (unsigned)v;
+    q[4 * h + 0] = __builtin_amdgcn_cvt_f32_fp8(v, 0) * (1.0f / kFp8Scale);
+    q[4 * h + 1] = __builtin_amdgcn_cvt_f32_fp8(v, 1) * (1.0f / kFp8Scale);
+    q[4 * h + 2] = __builtin_amdgcn_cvt_f32_fp8(v, 2) * (1.0f / kFp8Scale);
+    q[4 * h + 3] = __builtin_amdgcn_cvt_f32_fp8(v, 3) * (1.0f / kFp8Scale);
+  }
+  return r;
+}
+
+// Q8: also write the fp8 copy zq8 (row stride ldk8 bytes, zero padded to dk8) used by the fp8
+// forward GEMM; the positive logit then comes from the dequantised fp8 rows, consistent with
+// the GEMM's logits.
+template <typename Tin, typename Tc, bool Q8>
 __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
                                                    float* __restrict__ inv, float* __restrict__ ypos,
-                                                   int R, int d, int dk, int ldk, float y_scale) {
+                                                   int R, int d, int dk, int ldk, float y_scale,
+                                                   unsigned char* __restrict__ zq8, int dk8, int ldk8) {
   __shared__ float red[16];
   const int n = R >> 1, i = blockIdx.x, pi = i + n;
   const Tin* hi = h + (long long)i * d;
@@ -88,6 +110,8 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
   const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
   const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
   float dot = 0.f;
+  unsigned char* zi8 = Q8 ? zq8 + (long long)i * ldk8 : nullptr;
+  unsigned char* zp8 = Q8 ? zq8 + (long long)pi * ldk8 : nullptr;
   if (vec) {
     for (int e = threadIdx.x * 8; e < d; e += 256 * 8) {
       float a[8], b[8], qa[8], qb[8];
@@ -97,18 +121,33 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
       for (int j = 0; j < 8; ++j) { a[j] *= ivi; b[j] *= ivp; }
       store8<Tc>(zi + e, a, qa);
       store8<Tc>(zp + e, b, qb);
+      if constexpr (Q8) {
+        *reinterpret_cast<u32x2*>(zi8 + e) = quant8(a, qa);
+        *reinterpret_cast<u32x2*>(zp8 + e) = quant8(b, qb);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot += qa[j] * qb[j];
     }
   } else {
     for (int e = threadIdx.x; e < d; e += 256) {
-      const Tc a = from_f32<Tc>(to_f32<Tin>(hi[e]) * ivi);
-      const Tc b = from_f32<Tc>(to_f32<Tin>(hp[e]) * ivp);
+      const float af = to_f32<Tin>(hi[e]) * ivi, bf = to_f32<Tin>(hp[e]) * ivp;
+      const Tc a = from_f32<Tc>(af);
+      const Tc b = from_f32<Tc>(bf);
       zi[e] = a; zp[e] = b;
-      dot += to_f32<Tc>(a) * to_f32<Tc>(b);
+      if constexpr (Q8) {
+        const int va = __builtin_amdgcn_cvt_pk_fp8_f32(af * kFp8Scale, 0.f, 0, false);
+        const int vb = __builtin_amdgcn_cvt_pk_fp8_f32(bf * kFp8Scale, 0.f, 0, false);
+        zi8[e] = (unsigned char)(va & 0xFF);
+        zp8[e] = (unsigned char)(vb & 0xFF);
+        dot += __builtin_amdgcn_cvt_f32_fp8(va, 0) * __builtin_amdgcn_cvt_f32_fp8(vb, 0) * (1.0f / (kFp8Scale * kFp8Scale));
+      } else {
+        dot += to_f32<Tc>(a) * to_f32<Tc>(b);
+      }
     }
   }
   for (int e = d + threadIdx.x; e < dk; e += 256) { zi[e] = from_f32<Tc>(0.f); zp[e] = from_f32<Tc>(0.f); }
+  if constexpr (Q8)
+    for (int e = d + threadIdx.x; e < dk8; e += 256) { zi8[e] = 0; zp8[e] = 0; }
   dot = block_sum(dot, red);
   if (threadIdx.x == 0) {
     inv[i] = ivi; inv[pi] = ivp;
@@ -311,6 +350,23 @@ void dispatch_comp(DType t, F&& f) {
     case DType::F32: f(float{}); break;
     case DType::F16: f(_Float16{}); break;
     case DType::BF16: f(__bf16{}); break;
+    case DType::FP8: NTXENT_CHECK(false, "fp8 is a GEMM operand type only"); break;
+  }
+}
+
+// GEMM operand types (fp8 included).
+template <typename F>
+void dispatch_gemm(DType t, F&& f) {
+  if (t == DType::FP8) f(dev::fp8e4m3{});
+  else dispatch_comp(t, f);
+}
+
+// fp8 forward GEMMs: accumulators are products of e4m3(z * 256) values.
+void set_operand_scales(dev::SimParams& p, DType comp) {
+  if (comp == DType::FP8) {
+    const float inv2 = 1.0f / (dev::kFp8Scale * dev::kFp8Scale);
+    p.acc_scale = p.y_scale * inv2;
+    p.cos_scale = inv2;
   }
 }
 
@@ -370,6 +426,8 @@ dev::SimParams base_params(const Geometry& g) {
   p.row_tile0 = g.rank * g.row_tiles;
   p.col_tiles = g.col_tiles;
   p.y_scale = g.inv_temp * dev::kLog2e;
+  p.acc_scale = p.y_scale;
+  p.cos_scale = 1.0f;
   p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
   static const int dbg = [] {
     const char* e = std::getenv("NTXENT_GEMM_DEBUG");
@@ -440,6 +498,8 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
   g.dim_n = roundup(dim, kTile);
   g.ld_k = padded_ld(g.dim_k);
   g.ld_t = padded_ld(g.rows_pad);
+  g.dim_k8 = roundup(dim, 128);
+  g.ld_k8 = padded_ld(g.dim_k8);
   g.world = world;
   g.rank = rank;
   g.row_tiles = g.rows_pad / kTile;
@@ -536,20 +596,29 @@ std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit) {
 }
 
 void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
-                 const Geometry& g, hipStream_t stream) {
+                 const Geometry& g, hipStream_t stream, void* zq8) {
+  NTXENT_CHECK(comp != DType::FP8, "prep: pass the fp16 plan dtype and a zq8 buffer for fp8");
   const size_t cs = dtype_size(comp);
   if (g.rows_pad > g.rows) {
     NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq) + (size_t)g.rows * g.ld_k * cs, 0,
                                     (size_t)(g.rows_pad - g.rows) * g.ld_k * cs, stream));
+    if (zq8)
+      NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq8) + (size_t)g.rows * g.ld_k8, 0,
+                                      (size_t)(g.rows_pad - g.rows) * g.ld_k8, stream));
   }
   const float ys = g.inv_temp * dev::kLog2e;
   dispatch_comp(in, [&](auto tin) {
     using Tin = decltype(tin);
     dispatch_comp(comp, [&](auto tc) {
       using Tc = decltype(tc);
-      hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc>), dim3(g.rows / 2), dim3(256), 0, stream,
-                         static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
-                         g.dim_k, g.ld_k, ys);
+      if (zq8)
+        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, true>), dim3(g.rows / 2), dim3(256), 0, stream,
+                           static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
+                           g.dim_k, g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8);
+      else
+        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, false>), dim3(g.rows / 2), dim3(256), 0, stream,
+                           static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
+                           g.dim_k, g.ld_k, ys, nullptr, 0, 0);
     });
   });
   NTXENT_HIP_CHECK(hipGetLastError());
@@ -568,9 +637,11 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
                       hipStream_t stream) {
   if (ntiles == 0) return;
-  const long long kb = (long long)g.dim_k * dtype_size(comp);
-  const long long ld = (long long)g.ld_k * dtype_size(comp);
+  const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
+  const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
+  const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
+  set_operand_scales(p, comp);
   p.A = rowmajor_operand(zq_local, ld, kb);
   p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;
@@ -578,7 +649,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.part = part;
   p.sc = static_cast<char*>(sc);
   const int grid = apply_schedule(p, ntiles, ws, stream);
-  dispatch_comp(comp, [&](auto tc) {
+  dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
   });
@@ -589,9 +660,11 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
   if (ntiles == 0) return;
-  const long long kb = (long long)g.dim_k * dtype_size(comp);
-  const long long ld = (long long)g.ld_k * dtype_size(comp);
+  const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
+  const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
+  const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
+  set_operand_scales(p, comp);
   p.A = rowmajor_operand(zq_local, ld, kb);
   p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;
@@ -600,7 +673,7 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   p.lse2 = lse2_all;
   p.cpos = cpos;
   const int grid = apply_schedule(p, ntiles, ws, stream);
-  dispatch_comp(comp, [&](auto tc) {
+  dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeCoef>(grid, p, stream);
   });

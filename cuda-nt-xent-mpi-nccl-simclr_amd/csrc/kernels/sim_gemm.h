@@ -51,6 +51,8 @@ struct SimParams {
   long long kbytes;      // K bytes handled by one workgroup
   int R, Rpad, n_half, own0, row_tile0, col_tiles;
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
+  float acc_scale;       // logit (log2 units) per accumulator unit: y_scale, / kFp8Scale^2 for fp8
+  float cos_scale;       // cosine per accumulator unit: 1, or 1 / kFp8Scale^2 for fp8
   int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
   char* sc;              // kept cosines: [n_fwd_tiles][256*256] (canonical fragment order)
@@ -147,7 +149,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb
       const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
-        const float y = acc[mi][ni][r] * p.y_scale;
+        const float y = acc[mi][ni][r] * p.acc_scale;
         float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
         v = (gj[ni] == gpos) ? cpos4[r] : v;  // positive: -(a_i + a_p), no 1 - P cancellation
         v = (rvalid && cvalid[ni] && gj[ni] != gself) ? v : 0.0f;
@@ -522,20 +524,22 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       }
     }
   } else if constexpr (MODE == kModeCoef) {
-    coef_epilogue<T, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
+    coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
     const int kind = t.z;
     if (p.sc && !(p.dbg & kDbgNoStore)) {  // keep cosines (compact slot per tile, canonical order)
-      T* st = reinterpret_cast<T*>(p.sc) + (long long)tile * kTileElems;
+      typedef typename StoreT<T>::type TS;
+      TS* st = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
+      const float cs = p.cos_scale;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          T* dst = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
-          if constexpr (sizeof(T) == 2) {
-            union { T h[4]; u32x2 u; } pk;
+          TS* dst = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
+          if constexpr (sizeof(TS) == 2) {
+            union { TS h[4]; u32x2 u; } pk;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(acc[mi][ni][r]);
+            for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<TS>(acc[mi][ni][r] * cs);
             *reinterpret_cast<u32x2*>(dst) = pk.u;
           } else {
             *reinterpret_cast<f32x4*>(dst) = acc[mi][ni];
@@ -571,9 +575,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         for (int ni = 0; ni < 4; ++ni) {
           const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
           if (fixed)
-            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.y_scale - M) : 0.f;
+            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.acc_scale - M) : 0.f;
           else
-            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.y_scale : kNegInf;
+            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.acc_scale : kNegInf;
         }
       }
     float2* rowred = reinterpret_cast<float2*>(smem);                // [4 wb][256]

@@ -29,7 +29,10 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   rank_ = comm ? comm->rank() : 0;
   world_ = comm ? comm->world() : 1;
   g_ = make_geometry(cfg.rows, cfg.dim, world_, rank_, cfg.temperature);
-  cs_ = dtype_size(cfg.compute);
+  f8_ = cfg.compute == DType::FP8;
+  if (f8_) cfg_.keep_cos = true;  // fp8: the fp16 backward uses the forward's own cosines
+  bwd_ = backward_dtype(cfg.compute);
+  cs_ = dtype_size(bwd_);
 
   const auto ft = build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_, 1);
@@ -43,11 +46,12 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   struct Slot { void** p; size_t bytes; };
   const std::vector<Slot> slots = {
       {(void**)&zq_all_, W * Rp * g_.ld_k * cs_},
+      {(void**)&zq8_all_, f8_ ? W * Rp * g_.ld_k8 : 0},
       {(void**)&zqt_all_, W * g_.dim_n * g_.ld_t * cs_},
       {(void**)&inv_, R * 4},
       {(void**)&ypos_, R * 4},
       {(void**)&part_, (size_t)g_.col_tiles * Rp * sizeof(float2)},
-      {(void**)&sbuf_, cfg.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
+      {(void**)&sbuf_, cfg_.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
       {(void**)&cbuf_, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
       {(void**)&lse2_all_, W * Rp * 4},
       {(void**)&cpos_, Rp * 4},
@@ -100,17 +104,21 @@ void Engine::forward(const void* h, hipStream_t s) {
   const size_t Rp = g_.rows_pad;
   char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
   char* zqt_local = zqt_all_ + (size_t)rank_ * g_.dim_n * g_.ld_t * cs_;
+  // forward GEMM operand: the e4m3 rows for fp8 plans, else zq itself
+  char* op_all = f8_ ? zq8_all_ : zq_all_;
+  const size_t op_bytes = f8_ ? Rp * g_.ld_k8 : Rp * g_.ld_k * cs_;
+  char* op_local = op_all + (size_t)rank_ * op_bytes;
   {
     NTXENT_TRACE("ntxent.prep");
     fault_point("prep");
-    launch_prep(cfg_.input, cfg_.compute, h, zq_local, inv_, ypos_, g_, s);
-    launch_transpose(cfg_.compute, zq_local, zqt_local, g_, s);
+    launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
+    launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
     NTXENT_HIP_CHECK(hipEventRecord(ev_prep_, s));
     NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_prep_, 0));
-    comm_->all_gather(zq_local, zq_all_, Rp * g_.ld_k * cs_, comm_stream_);
+    comm_->all_gather(op_local, op_all, op_bytes, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zq_, comm_stream_));
     comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
@@ -119,12 +127,12 @@ void Engine::forward(const void* h, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
-    launch_fwd_stats(cfg_.compute, zq_local, zq_all_, fwd_tiles_, n_own_, part_, sbuf_, ws_, g_, s);
+    launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_, g_, s);
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");
     if (world_ > 1) NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zq_, 0));
-    launch_fwd_stats(cfg_.compute, zq_local, zq_all_, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
+    launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
                      sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_, g_, s);
   }
   {
@@ -149,7 +157,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");
     if (cfg_.keep_cos)
-      launch_coef(cfg_.compute, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s);
+      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s);
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s);
   }
@@ -160,7 +168,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.dz_gemm");
     fault_point("dz");
-    launch_dz(cfg_.compute, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s);
+    launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s);
   }
   {
     NTXENT_TRACE("ntxent.norm_bwd");

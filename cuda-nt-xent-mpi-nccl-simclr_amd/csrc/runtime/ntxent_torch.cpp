@@ -35,7 +35,7 @@ DType to_dtype(at::ScalarType t) {
 }
 
 at::ScalarType to_scalar(DType t) {
-  return t == DType::F32 ? at::kFloat : (t == DType::F16 ? at::kHalf : at::kBFloat16);
+  return t == DType::F32 ? at::kFloat : (t == DType::F16 ? at::kHalf : (t == DType::BF16 ? at::kBFloat16 : at::kByte));
 }
 
 // Compute-dtype policy. Normalised rows live in [-1, 1], where fp16's 10-bit mantissa beats
@@ -44,7 +44,8 @@ DType choose_compute(at::ScalarType in, bool use_mixed_precision, const std::str
   if (override_ == "fp32" || override_ == "float32") return DType::F32;
   if (override_ == "fp16" || override_ == "float16") return DType::F16;
   if (override_ == "bf16" || override_ == "bfloat16") return DType::BF16;
-  NTXENT_CHECK(override_.empty() || override_ == "auto", "compute_dtype must be auto|fp32|fp16|bf16");
+  if (override_ == "fp8" || override_ == "float8") return DType::FP8;
+  NTXENT_CHECK(override_.empty() || override_ == "auto", "compute_dtype must be auto|fp32|fp16|bf16|fp8");
   if (in == at::kFloat && !use_mixed_precision) return DType::F32;
   return DType::F16;
 }
@@ -74,6 +75,9 @@ struct Plan {
   int col_tiles() const { return g.col_tiles; }
   double temperature() const { return g.temperature; }
   std::string compute_dtype() const { return dtype_name(comp); }
+  DType bwd() const { return backward_dtype(comp); }                  // zq / sc / C / ZqT dtype
+  long op_ld() const { return comp == DType::FP8 ? g.ld_k8 : g.ld_k; }  // forward operand row stride
+  std::string backward_dtype_name() const { return dtype_name(bwd()); }
 };
 
 static at::Tensor upload_tiles(const std::vector<int4>& v, int device) {
@@ -148,7 +152,10 @@ static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) 
 // ---- stage ops ----------------------------------------------------------------------
 // `zq_out` (optional): write the normalised rows into this [rows_pad, ld_k] buffer — e.g. this
 // rank's slot of the all-gather destination, so the gather runs in place.
-std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::optional<at::Tensor>& zq_out) {
+// Returns {zq, inv, ypos, zq8}: zq in the backward dtype; zq8 (uint8 e4m3 rows [rows_pad, ld_k8])
+// only for fp8 plans (undefined otherwise), written into `zq8_out` when given.
+std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::optional<at::Tensor>& zq_out,
+                             const c10::optional<at::Tensor>& zq8_out) {
   check_input(h, "h");
   NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
   const at::DeviceGuard guard(h.device());
@@ -156,16 +163,27 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::opti
   if (zq_out.has_value() && zq_out->defined()) {
     zq = *zq_out;
     check_input(zq, "zq_out");
-    NTXENT_CHECK(zq.numel() == (long)P.g.rows_pad * P.g.ld_k && zq.scalar_type() == to_scalar(P.comp),
-                 "zq_out must be [rows_pad, ld_k] in the compute dtype");
+    NTXENT_CHECK(zq.numel() == (long)P.g.rows_pad * P.g.ld_k && zq.scalar_type() == to_scalar(P.bwd()),
+                 "zq_out must be [rows_pad, ld_k] in the backward dtype");
   } else {
-    zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.comp)));
+    zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())));
+  }
+  at::Tensor zq8;
+  if (P.comp == DType::FP8) {
+    if (zq8_out.has_value() && zq8_out->defined()) {
+      zq8 = *zq8_out;
+      check_input(zq8, "zq8_out");
+      NTXENT_CHECK(zq8.numel() == (long)P.g.rows_pad * P.g.ld_k8 && zq8.scalar_type() == at::kByte,
+                   "zq8_out must be uint8 [rows_pad, ld_k8]");
+    } else {
+      zq8 = at::empty({P.g.rows_pad, P.g.ld_k8}, opts(h, at::kByte));
+    }
   }
   auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
   auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
-  launch_prep(to_dtype(h.scalar_type()), P.comp, h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(),
-              ypos.data_ptr<float>(), P.g, cur_stream(h));
-  return {zq, inv, ypos};
+  launch_prep(to_dtype(h.scalar_type()), P.bwd(), h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(),
+              ypos.data_ptr<float>(), P.g, cur_stream(h), zq8.defined() ? zq8.data_ptr() : nullptr);
+  return {zq, inv, ypos, zq8};
 }
 
 at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at::Tensor>& zqt_out) {
@@ -180,7 +198,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
   } else {
     zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
   }
-  launch_transpose(P.comp, zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
+  launch_transpose(P.bwd(), zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
 }
 
@@ -188,12 +206,12 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
                                   bool keep_cos) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
-  NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.g.ld_k,
-               "zq_all must be [world*rows_pad, ld_k]");
+  NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.op_ld(),
+               "zq_all must be [world*rows_pad, ld] in the forward operand dtype (ld_k, or ld_k8 for fp8)");
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, zq_local.options());
+  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -213,13 +231,14 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   NTXENT_CHECK(first >= 0 && count >= 0 && first + count <= P.n_fwd, "tile range out of bounds");
   NTXENT_CHECK(part.numel() == (long)P.g.col_tiles * P.g.rows_pad * 2 && part.scalar_type() == at::kFloat,
                "part must be float32 [col_tiles, rows_pad, 2]");
-  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.g.ld_k, "zq_all must be [world*rows_pad, ld_k]");
+  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.op_ld(),
+               "zq_all must be [world*rows_pad, ld] in the forward operand dtype");
   const bool keep = sc.has_value() && sc->defined();
   if (keep) NTXENT_CHECK(sc->numel() == (long)P.n_fwd * kTileElems, "sc must hold n_fwd tiles");
   if (count == 0) return;
   const at::DeviceGuard guard(zq_local.device());
   auto ws = gemm_ws(zq_local, count, P);
-  char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.comp) : nullptr;
+  char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local));
@@ -248,7 +267,7 @@ at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Te
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
-  launch_coef(P.comp, sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
+  launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf));
   return cbuf;
 }
@@ -257,7 +276,7 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
                      const at::Tensor& cpos, const Plan& P) {
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
-  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, zq_local.options());
+  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -272,7 +291,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   const at::DeviceGuard guard(sc.device());
   auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
   auto ws = gemm_ws(sc, P.n_dz, P);
-  launch_dz(P.comp, sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
+  launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, slabs.data_ptr<float>(), ws, P.g, cur_stream(sc));
   return slabs;
 }
@@ -299,9 +318,12 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   // callers as an explicit "fp16".
   const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
-  auto pr = prep(h, *P, c10::nullopt);
+  auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
   auto zqt = transpose(pr[0], *P, c10::nullopt);
-  auto fs = fwd_stats(pr[0], pr[0], *P, keep_cos);
+  // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
+  // the fp16 backward uses exactly the forward's logits
+  const bool f8 = comp == DType::FP8;
+  auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
@@ -349,7 +371,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   const at::DeviceGuard guard(z.device());
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
-  auto pr = prep(z, *P, c10::nullopt);
+  auto pr = prep(z, *P, c10::nullopt, c10::nullopt);
   auto zqt = transpose(pr[0], *P, c10::nullopt);
   auto lse2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
@@ -428,6 +450,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("col_tiles", &Plan::col_tiles)
       .def_property_readonly("temperature", &Plan::temperature)
       .def_property_readonly("compute_dtype", &Plan::compute_dtype)
+      .def_property_readonly("backward_dtype", &Plan::backward_dtype_name)
+      .def_property_readonly("ld_k8", [](const Plan& p) { return p.g.ld_k8; })
       .def_readonly("n_fwd_tiles", &Plan::n_fwd)
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
@@ -440,7 +464,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     at::ScalarType t = in_dtype == "float32" ? at::kFloat : (in_dtype == "float16" ? at::kHalf : at::kBFloat16);
     return std::string(ntxent::dtype_name(choose_compute(t, mp, ov)));
   });
-  m.def("prep", &prep, py::arg("h"), py::arg("plan"), py::arg("zq_out") = py::none());
+  m.def("prep", &prep, py::arg("h"), py::arg("plan"), py::arg("zq_out") = py::none(), py::arg("zq8_out") = py::none());
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"));

@@ -22,7 +22,7 @@ import torch
 
 from . import _ext, reference
 
-_VALID_COMPUTE = ("auto", "fp32", "fp16", "bf16")
+_VALID_COMPUTE = ("auto", "fp32", "fp16", "bf16", "fp8")
 
 
 def _use_reference(h: torch.Tensor) -> bool:
@@ -73,7 +73,10 @@ def ntxent_loss(h: torch.Tensor, temperature: float = 0.07, *, use_mixed_precisi
     Args:
       temperature: tau.
       use_mixed_precision: fp32 inputs are computed in fp16 (fp32 accumulate) if True.
-      compute: override the compute dtype: ``auto|fp32|fp16|bf16``.
+      compute: override the compute dtype: ``auto|fp32|fp16|bf16|fp8``. ``fp8`` runs the forward
+        similarity GEMM on e4m3 MFMA (per-tensor scale 256) and the backward in fp16; the
+        loss is that of the fp8-quantised rows (logit error ~1e-2 at tau=0.07, see
+        tests/test_gpu_fp8.py).
       keep_logits: keep the cosine tiles (compute dtype) between forward and backward
         (default; saves one similarity GEMM). False recomputes them in the backward.
     """
@@ -86,7 +89,7 @@ def ntxent_loss(h: torch.Tensor, temperature: float = 0.07, *, use_mixed_precisi
             raise RuntimeError("NTXENT_FORCE_REFERENCE requires NTXENT_ALLOW_REFERENCE=1")
         return reference.ntxent_loss(h, temperature)
     comp = resolve_compute(h.dtype, use_mixed_precision, compute)
-    return NTXentFunction.apply(h, float(temperature), comp, bool(keep_logits))
+    return NTXentFunction.apply(h, float(temperature), comp, bool(keep_logits) or comp == "fp8")
 
 
 class NTXentLoss(torch.nn.Module):

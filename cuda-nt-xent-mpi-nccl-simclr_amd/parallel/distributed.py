@@ -43,17 +43,22 @@ class DistNTXentFunction(torch.autograd.Function):
         R, d = h.shape
         plan = C.get_plan(R, d, W, r, float(temperature), compute, h.device.index)
         Rpad = plan.rows_pad
-        cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[plan.compute_dtype]
+        f8 = plan.compute_dtype == "fp8"
+        keep_logits = keep_logits or f8  # fp8 plans always keep their (fp16) cosines
+        cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[plan.backward_dtype]
         # prep / transpose write straight into this rank's slot: the gathers run in place.
         zq_all = torch.empty((W * Rpad, plan.ld_k), dtype=cdt, device=h.device)
         zqt_all = torch.empty((W, plan.dim_n, plan.ld_t), dtype=cdt, device=h.device)
         zq = zq_all[r * Rpad:(r + 1) * Rpad]
         zqt = zqt_all[r]
-        _, inv, ypos = C.prep(h, plan, zq)
+        # fp8: the forward GEMM (and so the forward gather) uses the 1-byte e4m3 rows
+        fwd_all = torch.empty((W * Rpad, plan.ld_k8), dtype=torch.uint8, device=h.device) if f8 else zq_all
+        fwd = fwd_all[r * Rpad:(r + 1) * Rpad]
+        _, inv, ypos, _ = C.prep(h, plan, zq, fwd if f8 else None)
         C.transpose(zq, plan, zqt)
         work_z = work_t = None
         if W > 1:
-            work_z = dist.all_gather_into_tensor(zq_all, zq, group=group, async_op=True)
+            work_z = dist.all_gather_into_tensor(fwd_all, fwd, group=group, async_op=True)
             work_t = dist.all_gather_into_tensor(zqt_all, zqt, group=group, async_op=True)
             if not overlap:
                 work_z.wait()
@@ -61,10 +66,10 @@ class DistNTXentFunction(torch.autograd.Function):
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=h.device)
         sc = torch.empty((plan.n_fwd_tiles * 256 * 256,), dtype=cdt, device=h.device) if keep_logits else None
         # own-rank (upper-triangular) tiles need only this rank's slot: they overlap the gather
-        C.fwd_stats_range(zq, zq_all, plan, part, sc, 0, plan.n_own_tiles)
+        C.fwd_stats_range(fwd, fwd_all, plan, part, sc, 0, plan.n_own_tiles)
         if work_z is not None:
             work_z.wait()
-        C.fwd_stats_range(zq, zq_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles)
+        C.fwd_stats_range(fwd, fwd_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles)
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
@@ -89,7 +94,7 @@ class DistNTXentFunction(torch.autograd.Function):
             ctx.work_t = None
         sc, ctx.sc = ctx.sc, None
         if ctx.backward_mode == "reduce_scatter":
-            dh = _reduce_scatter_backward(ctx.plan, h, zq, zq_all, inv, lse2_all, grad_out, ctx.group)
+            dh = _reduce_scatter_backward(ctx.plan, h, zq, zqt_all, inv, lse2_all, grad_out, ctx.group)
             return dh, None, None, None, None, None, None
         if sc is not None:
             sc = C.coef(sc, lse2_all, cpos, ctx.plan)
@@ -100,7 +105,7 @@ class DistNTXentFunction(torch.autograd.Function):
         return dh, None, None, None, None, None, None
 
 
-def _reduce_scatter_backward(plan, h, zq, zq_all, inv, lse2_all, grad_out, group):
+def _reduce_scatter_backward(plan, h, zq, zqt_all, inv, lse2_all, grad_out, group):
     """Comparison variant named by the north star: each rank differentiates only ITS loss terms
     w.r.t. ALL gathered rows (row part locally, column part G_cols = D^T z_local for every
     global row) and a reduce-scatter sums the column parts onto their owners.
@@ -116,7 +121,8 @@ def _reduce_scatter_backward(plan, h, zq, zq_all, inv, lse2_all, grad_out, group
     n = R // 2
     T = plan.temperature
     z = zq[:R, :d].float()
-    rows_all = torch.cat([zq_all[q * Rpad:q * Rpad + R, :d] for q in range(W)], 0).float()  # [W*R, d]
+    # every rank's rows from the gathered transposes (gathered in every precision mode)
+    rows_all = torch.cat([zqt_all[q, :d, :R].t() for q in range(W)], 0).float()  # [W*R, d]
     S = z @ rows_all.t() / T
     ar = torch.arange(R, device=h.device)
     S[ar, ar + r * R] = float("-inf")

@@ -30,16 +30,21 @@ def emulated_dist_forward_backward(shards: Sequence[torch.Tensor], temperature: 
     plans = [C.get_plan(R, d, W, r, float(temperature), comp, dev.index) for r in range(W)]
     P0 = plans[0]
     Rpad = P0.rows_pad
-    cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[P0.compute_dtype]
+    f8 = P0.compute_dtype == "fp8"
+    keep_logits = keep_logits or f8  # fp8 plans always keep their (fp16) cosines
+    cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[P0.backward_dtype]
     zq_all = torch.empty((W * Rpad, P0.ld_k), dtype=cdt, device=dev)
     zqt_all = torch.empty((W, P0.dim_n, P0.ld_t), dtype=cdt, device=dev)
+    zq8_all = torch.empty((W * Rpad, P0.ld_k8), dtype=torch.uint8, device=dev) if f8 else None
     invs, yposs = [], []
     for r in range(W):  # "all-gather" of Zq / ZqT: every rank writes its own slot
         zq = zq_all[r * Rpad:(r + 1) * Rpad]
-        _, inv, ypos = C.prep(shards[r].contiguous(), plans[r], zq)
+        zq8 = zq8_all[r * Rpad:(r + 1) * Rpad] if f8 else None
+        _, inv, ypos, _ = C.prep(shards[r].contiguous(), plans[r], zq, zq8)
         C.transpose(zq, plans[r], zqt_all[r])
         invs.append(inv)
         yposs.append(ypos)
+    fwd_all = zq8_all if f8 else zq_all  # forward GEMM operand
     lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=dev)
     loss = torch.zeros((), dtype=torch.float32, device=dev)
     scs, cposs = [], []
@@ -47,8 +52,7 @@ def emulated_dist_forward_backward(shards: Sequence[torch.Tensor], temperature: 
         P = plans[r]
         part = torch.empty((P.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         sc = torch.empty((P.n_fwd_tiles * 256 * 256,), dtype=cdt, device=dev) if keep_logits else None
-        zq = zq_all[r * Rpad:(r + 1) * Rpad]
-        C.fwd_stats_range(zq, zq_all, P, part, sc, 0, P.n_fwd_tiles)
+        C.fwd_stats_range(fwd_all[r * Rpad:(r + 1) * Rpad], fwd_all, P, part, sc, 0, P.n_fwd_tiles)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=dev)
         loss = loss + C.lse(part, yposs[r], lse2_all, cpos, P)  # "all-gather" of LSE + "all-reduce"
         scs.append(sc)
