@@ -17,6 +17,7 @@
 #include "sim_gemm.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -559,6 +560,15 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   GemmSchedule s;
   s.nk = nk;
   s.grid = std::max(1, std::min(num_cus, ntiles * nk));
+  if (ntiles < s.grid) {
+    // Fewer tiles than CUs: every tile is split into p K-pieces. The last-arriving piece sums
+    // p fp32 partial tiles (256 KiB each, ~5 us per slab for one CU) while a piece saves
+    // nk/p K-steps (~2 us each), so p ~ sqrt(0.4 nk) balances them; splitting across all CUs
+    // instead (p = G/ntiles) made a small-batch dZ GEMM sum 32 slabs serially.
+    const int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
+    const int p = std::max(1, std::min(p_opt, s.grid / std::max(1, ntiles)));
+    s.grid = std::max(1, ntiles * p);
+  }
   const int G = s.grid;
   const int full = ntiles / G, rem = ntiles % G;
   if (rem == 0) {
