@@ -412,10 +412,76 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
       std::fprintf(stderr, "\n");
       return;
     }
+    case 64: {  // per-block item timeline of every block, summarised to stderr (synchronising)
+      static unsigned long long* buf = nullptr;
+      static int cap = 0;
+      if (cap < grid) {
+        if (buf) NTXENT_HIP_CHECK(hipFree(buf));
+        NTXENT_HIP_CHECK(hipMalloc(&buf, (size_t)grid * 64 * 8));
+        cap = grid;
+      }
+      NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, (size_t)grid * 64 * 8, stream));
+      dev::SimParams q = p;
+      q.stamps = buf;
+      hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 64>), dim3(grid), dim3(kGemmThreads), 0, stream, q);
+      std::vector<unsigned long long> h((size_t)grid * 64);
+      NTXENT_HIP_CHECK(hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, stream));
+      NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
+      unsigned long long t0 = ~0ull, t1 = 0;
+      double clk = 0, loop_full = 0, n_full = 0, loop_part = 0, steps_part = 0, pro = 0, fix = 0, epi = 0, tail = 0;
+      double n_items = 0, n_fix = 0, busy_max = 0, start_max = 0;
+      double ep[5] = {0, 0, 0, 0, 0};  // fwd epilogue phases: store, masks, exp+reduce, barrier, merge
+      for (int b = 0; b < grid; ++b) {
+        const unsigned long long* s = h.data() + (size_t)b * 64;
+        t0 = std::min(t0, s[0]);
+        t1 = std::max(t1, s[2]);
+        clk += (double)(s[2] - s[0]) / (double)std::max(1ull, s[3] - s[1]) * 0.1;  // GHz (100 MHz ref)
+      }
+      for (int b = 0; b < grid; ++b) {
+        const unsigned long long* s = h.data() + (size_t)b * 64;
+        start_max = std::max(start_max, (double)(s[0] - t0));
+        busy_max = std::max(busy_max, (double)(s[2] - s[0]));
+        tail += (double)(t1 - s[2]);
+        for (int k = 0; k < 9 && s[6 + 6 * k]; ++k) {
+          const unsigned long long* it = s + 4 + 6 * k;
+          const double loop = (double)(it[3] - it[2]);
+          if ((int)it[1] == p.nk) { loop_full += loop; n_full += 1; }
+          else { loop_part += loop; steps_part += (double)it[1]; }
+          fix += (double)(it[4] - it[3]);
+          n_fix += (int)it[1] != p.nk;
+          if (it[5]) epi += (double)(it[5] - it[4]);
+          if (it[5] && k < 6 && s[40 + 4 * k]) {
+            const unsigned long long* e = s + 40 + 4 * k;
+            ep[0] += (double)(e[0] - it[4]); ep[1] += (double)(e[1] - e[0]); ep[2] += (double)(e[2] - e[1]);
+            ep[3] += (double)(e[3] - e[2]); ep[4] += (double)(it[5] - e[3]);
+          }
+          n_items += 1;
+          // gap between the previous item's end and this one's start (loop bookkeeping)
+          pro += (double)(it[2] - (k == 0 ? s[0] : s[4 + 6 * (k - 1) + 5] ? s[4 + 6 * (k - 1) + 5] : s[4 + 6 * (k - 1) + 4]));
+        }
+      }
+      clk /= grid;
+      const double us = 1e-3 / clk;  // microseconds per cycle
+      std::fprintf(stderr,
+                   "TIMELINE mode=%d grid=%d nk=%d dp=%d sk=%d ipb=%lld clk=%.3fGHz span=%.1fus start_skew=%.1fus "
+                   "busy_max=%.1fus | per block: items=%.2f loop_full=%.1fus (%.0f cyc/kstep, %d tiles) "
+                   "loop_part=%.1fus (%.0f cyc/kstep) fixup=%.1fus epilogue=%.1fus [store %.1f masks %.1f exp %.1f "
+                   "bar %.1f merge %.1f] gaps=%.1fus tail_idle=%.1fus\n",
+                   MODE, grid, p.nk, p.dp_tiles, p.sk_tiles, p.ipb, clk, (t1 - t0) * us, start_max * us, busy_max * us,
+                   n_items / grid, loop_full / grid * us, n_full ? loop_full / n_full / p.nk : 0.0, (int)n_full,
+                   loop_part / grid * us, steps_part ? loop_part / steps_part : 0.0, fix / grid * us, epi / grid * us,
+                   ep[0] / grid * us, ep[1] / grid * us, ep[2] / grid * us, ep[3] / grid * us, ep[4] / grid * us,
+                   pro / grid * us, tail / grid * us);
+      return;
+    }
     default: break;
   }
 #endif
-  hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
+  if (MODE == dev::kModeFwd && !p.fixed_shift)
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 0, MODE == dev::kModeFwd ? 0 : 1>), dim3(grid), dim3(kGemmThreads), 0,
+                       stream, p);
+  else
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
 }
 
 dev::SimParams base_params(const Geometry& g) {
@@ -557,32 +623,30 @@ int choose_dz_ksplit(const Geometry& g, int num_cus) {
 }
 
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
+  // Whole tiles in data-parallel rounds of G = num_cus blocks; only the remainder tiles
+  // (ntiles % G) are split, into p K-pieces each, run by the first rem * p blocks after their
+  // DP rounds. A split tile costs its contributors a 256 KiB fp32 partial slab each and its
+  // last arriver p - 1 slab reads (~5 us per slab for one CU), while a piece saves nk/p
+  // K-steps (~2 us each), so p ~ sqrt(0.4 nk). The classic hybrid (one DP round fewer, that
+  // round plus the remainder split over every block) balanced K-steps exactly but split
+  // ~G + rem tiles: the forward GEMM at B = 4096 spent 30-74 us per block in slab traffic,
+  // the whole chip publishing at once. Splitting across all CUs when tiles < CUs
+  // (p = G / ntiles) made a small-batch dZ GEMM sum 32 slabs serially.
   GemmSchedule s;
   s.nk = nk;
-  s.grid = std::max(1, std::min(num_cus, ntiles * nk));
-  if (ntiles < s.grid) {
-    // Fewer tiles than CUs: every tile is split into p K-pieces. The last-arriving piece sums
-    // p fp32 partial tiles (256 KiB each, ~5 us per slab for one CU) while a piece saves
-    // nk/p K-steps (~2 us each), so p ~ sqrt(0.4 nk) balances them; splitting across all CUs
-    // instead (p = G/ntiles) made a small-batch dZ GEMM sum 32 slabs serially.
-    const int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
-    const int p = std::max(1, std::min(p_opt, s.grid / std::max(1, ntiles)));
-    s.grid = std::max(1, ntiles * p);
-  }
-  const int G = s.grid;
-  const int full = ntiles / G, rem = ntiles % G;
+  const int G0 = std::max(1, num_cus);
+  const int q = ntiles / G0, rem = ntiles % G0;
+  s.dp_tiles = q * G0;
+  s.sk_tiles = rem;
   if (rem == 0) {
-    s.dp_tiles = ntiles;
-    s.sk_tiles = 0;
-  } else if (full == 0) {
-    s.dp_tiles = 0;
-    s.sk_tiles = ntiles;
-  } else {  // data-parallel rounds, then one round + the remainder shared by stream-K
-    s.dp_tiles = (full - 1) * G;
-    s.sk_tiles = ntiles - s.dp_tiles;
+    s.grid = std::min(G0, std::max(1, ntiles));
+    s.ipb = 0;
+    return s;
   }
-  s.ipb = ((long long)s.sk_tiles * nk + G - 1) / G;
-  if (s.sk_tiles == 0) s.ipb = 0;
+  const int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
+  const int p = std::max(1, std::min({p_opt, G0 / rem, nk}));
+  s.grid = q > 0 ? G0 : rem * p;
+  s.ipb = (nk + p - 1) / p;  // K-steps per stream-K block; ceil(rem * nk / ipb) <= rem * p blocks busy
   return s;
 }
 

@@ -25,6 +25,8 @@
 #include "../include/ntxent/ntxent.h"
 #include "device_common.h"
 
+#include <type_traits>
+
 namespace ntxent {
 namespace dev {
 
@@ -72,6 +74,12 @@ struct SimParams {
   float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
   int* sk_cnt;           // [sk_tiles] arrival counters (zero at launch; self-cleaning)
 };
+
+// Kept-cosine layout for 2-byte types: one 16-byte unit per lane holds the fragments of the
+// 16-column blocks cb and cb + 16 (cb a multiple of 32) of the 16-row block at rb (4 values
+// each, MFMA C layout). Element offset of the unit = sc_unit(...) * 8. fp32 tiles keep one
+// fragment per 16-byte unit: (((rb >> 4) * 16 + (cb >> 4)) * 64 + lane) * 4.
+__device__ __forceinline__ int sc_unit(int rb, int cb, int lane) { return ((rb >> 4) * 8 + (cb >> 5)) * 64 + lane; }
 
 // Ablation bits (timing experiments only; results are garbage when set).
 constexpr int kDbgNoLoads = 1;     // skip the global->LDS staging in the main loop
@@ -221,7 +229,9 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb
 // ABL: compile-time ablations for diagnostic builds only (production instantiates ABL = 0):
 // 1 = no global->LDS DMA, 2 = no LDS operand reads, 4 = no MFMA, 8 = deeper DMA queue,
 // 16 = no barriers (8 and 16 only make sense with 2|4), 32 = clock stamps (tools/ablate_ct.sh).
-template <typename T, int MODE, int ABL = 0>
+// FX: the forward epilogue's exponential form, fixed shift (1, tau > ~0.024) or per-tile max
+// (0). A compile-time choice: with both forms in one kernel the allocator spilled the main loop.
+template <typename T, int MODE, int ABL = 0, int FX = 1>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
@@ -373,6 +383,21 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const long long it1 = it0 + p.ipb < sk_total ? it0 + p.ipb : sk_total;
   const int n_dp = p.dp_tiles > bid ? (p.dp_tiles - bid + G - 1) / G : 0;
   long long it = it0;
+  // ABL & 64: per-block item timeline (diagnostic builds). 64 slots per block: [0] memtime and
+  // [1] memrealtime at entry, [2]/[3] the same at exit; item k at 4 + 6k: tile, K-steps, then
+  // memtime at item start, main-loop end, stream-K fixup end, epilogue end.
+  unsigned long long* tl = (ABL & 64) ? p.stamps + (size_t)bid * 64 : nullptr;
+  // (the clock reads happen only inside the constexpr branch: production code is unchanged)
+  auto tval = [&](int slot, unsigned long long v) {
+    if constexpr ((ABL & 64) != 0) {
+      if (threadIdx.x == 0 && slot < 64) tl[slot] = v;
+    }
+  };
+  auto tstamp = [&](int slot) {
+    if constexpr ((ABL & 64) != 0) tval(slot, __builtin_amdgcn_s_memtime());
+  };
+  if constexpr ((ABL & 64) != 0) tval(1, __builtin_amdgcn_s_memrealtime());
+  tstamp(0);
   for (int item = 0;; ++item) {
   int tile, kb, ke, stile = -1;
   long long seg0 = 0;
@@ -392,6 +417,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const int4 t = p.tiles[tile];
   const int mt = t.x, nt = t.y;
   const int nsteps = ke - kb;
+  tval(4 + 6 * item, (unsigned long long)tile);
+  tval(5 + 6 * item, (unsigned long long)nsteps);
+  tstamp(6 + 6 * item);
   Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
   Bb = p.B.base + (long long)nt * p.B.row_tile_stride;
   {
@@ -439,6 +467,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if (grp == 0) barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
   __syncthreads();
+  tstamp(7 + 6 * item);
   {
   // Thread indices re-derived through an opaque copy: keeps the compiler from hoisting the
   // epilogue's address arithmetic out of the persistent loop, where it would stay live across
@@ -455,54 +484,71 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   if (nsteps != nk) {
     // ---- stream-K fixup: partial K-range of tile `stile` -------------------------------
-    // Publish the fp32 partial (canonical fragment order, 256 KiB) with plain stores, drain,
-    // agent-scope release, then count arrivals (cdna_hip_programming.md §5, split-K recipe).
-    // The last arriver acquires and re-sums ALL segments in block order (deterministic).
+    // Publish the fp32 partial (fragment order, 256 KiB) with write-through (sc1) 16-B
+    // stores, drain every wave, then one lane counts the arrival. The last arriver sums the
+    // segments in block order with sc1 loads (MI355X_MICROARCH.md § visibility, Valid forms
+    // row 1: sc1 payload both sides + ticket, so neither an agent release — whose L2
+    // write-back of every dirty line of the XCD cost ~30 us per episode here — nor an
+    // acquire). Its own segment stays in registers: fp32 addition is commutative, so
+    // ((s_b0 + s_b1) + s_b2) ... comes out bitwise identical whoever arrives last.
     const int b0 = (int)((long long)stile * nk / p.ipb);
     const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
-    auto slot_of = [&](int bb) {
+    auto slot_off = [&](int bb) {  // byte offset of block bb's slab for this tile
       const long long s = (long long)bb * p.ipb;
       const bool first_partial = (s / nk == stile) && (s % nk != 0);
-      return p.sk_slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
+      return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
     };
     (void)seg0;
-    float* mine = slot_of(bid);
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
+    const unsigned lane_off = (unsigned)((w * 32 * 64 + lane) * 16);
+    {
+      const unsigned mine = slot_off(bid) + lane_off;
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-        *reinterpret_cast<f32x4*>(mine + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4) = acc[mi][ni];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int f = 0; f < 32; ++f) {
+        const f32x4 a = acc[f >> 2][f & 3];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), srs, (int)(mine + f * 64 * 16), 0, 16);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == b1 - b0;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // every contributor has arrived: return the counter to zero for the next launch
-        __hip_atomic_store(p.sk_cnt + stile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      // every contributor has arrived: return the counter to zero for the next launch
+      if (last) __hip_atomic_store(p.sk_cnt + stile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = last;
     }
     __syncthreads();
     const bool last = flag[0] != 0;
     __syncthreads();
-    if (!last) continue;
-    for (int bb = b0; bb <= b1; ++bb) {
-      const float* src = slot_of(bb);
+    if (!last) {
+      tstamp(8 + 6 * item);
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    // The own segment stays in registers when it is the first or second term of the sum
+    // ((s_b0 + s_me) = (s_me + s_b0) bitwise); a later position re-reads it from its slab.
+    const bool reload_all = bid - b0 >= 2;
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
+    for (int g = 0; g < 4; ++g) {
+      for (int bb = b0; bb <= b1; ++bb) {
+        if (bb == bid && !reload_all) continue;
+        const unsigned off = slot_off(bb) + lane_off;
+        u32x4 v[8];
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(src + ((w * 32 + mi * 4 + ni) * 64 + lane) * 4);
-          acc[mi][ni] = (bb == b0) ? v : acc[mi][ni] + v;
+        for (int j = 0; j < 8; ++j)
+          v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(off + (g * 8 + j) * 64 * 16), 0, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
+          f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
+          a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
         }
+      }
     }
   }
+  tstamp(8 + 6 * item);
 
   if (p.dbg & kDbgNoEpilogue) {  // timing ablation: keep the MFMA results live, write nothing
     float s = 0.f;
@@ -534,15 +580,23 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          TS* dst = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
+        for (int np = 0; np < 2; ++np) {
           if constexpr (sizeof(TS) == 2) {
-            union { TS h[4]; u32x2 u; } pk;
+            // 16-B stores (half the store-issue time of 8-B ones): the fragments of the column
+            // blocks cb and cb + 16 share one unit, see sc_unit()
+            union { TS h[8]; u32x4 u; } pk;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<TS>(acc[mi][ni][r] * cs);
-            *reinterpret_cast<u32x2*>(dst) = pk.u;
+            for (int r = 0; r < 4; ++r) {
+              pk.h[r] = from_f32<TS>(acc[mi][2 * np][r] * cs);
+              pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r] * cs);
+            }
+            *reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8) = pk.u;
           } else {
-            *reinterpret_cast<f32x4*>(dst) = acc[mi][ni];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              const int ni = 2 * np + q;
+              *reinterpret_cast<f32x4*>(st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4) = acc[mi][ni];
+            }
           }
         }
     }
@@ -555,55 +609,89 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     // max passes). Smaller tau falls back to per-tile max shifting (2 exps per element).
     const int col_local0 = (nt * kTile) % p.Rpad;
     const bool own_blk = kind != kTilePlain;
-    const bool fixed = p.fixed_shift != 0;
+    constexpr bool fixed = FX != 0;  // launch_sim_gemm picks FX = p.fixed_shift
     const float M = p.y_scale;
-    bool cvalid[4];
-    int cloc[4];
+    if (item < 6) tstamp(40 + 4 * item);  // ABL & 64: epilogue phases (cosines stored)
+    // Masks, as a pre-pass that sets the masked raw values to -inf (exp2 -> 0). Element
+    // (tile row tr, tile col tc) is the self pair when tc - tr == r0 - c0 and a positive when
+    // tc - tr == r0 - c0 +- n_half; a 16x16 fragment can hold such an element only if its block
+    // offset cb - rb is within 15 of that difference, and padding only at the tile edge. These
+    // tests are wave-uniform, so only the few fragments that need it run per-lane selects; the
+    // per-element masked form compiled to per-element control flow (~15 us per tile) and the
+    // fully unrolled select form spilled the main loop.
+    {
+      const int r0 = mt * kTile, c0 = col_local0;
+      const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+      const bool pad = (r0 + kTile > p.R) || (c0 + kTile > p.R);
+      if (own_blk || pad) {
+        // block offsets from the wave index in an SGPR: the tests compile to scalar branches
+        const int ws = __builtin_amdgcn_readfirstlane(w);
+        const int was = ws >> 2, wbs = ws & 3;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      cloc[ni] = col_local0 + cb[ni] + (lane & 15);
-      cvalid[ni] = cloc[ni] < p.R;
-    }
+        for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+          for (int ni = 0; ni < 4; ++ni) {
+            const int rbs = 128 * (mi >> 2) + 64 * was + 16 * (mi & 3);
+            const int cbs = 128 * (ni >> 1) + 32 * wbs + 16 * (ni & 1);
+            const int off = cbs - rbs;
+            const bool near = own_blk && ((off - D0 <= 15 && D0 - off <= 15) || (off - D1 <= 15 && D1 - off <= 15) ||
+                                          (off - D2 <= 15 && D2 - off <= 15));
+            const bool edge = (r0 + rbs + 16 > p.R) || (c0 + cbs + 16 > p.R);
+            if (near || edge) {
+              const int tc = cb[ni] + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = mt * kTile + rb[mi] + 4 * (lane >> 4) + r;
-        const bool rvalid = gi < p.R;
-        const int lpos = gi < p.n_half ? gi + p.n_half : gi - p.n_half;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const bool ok = rvalid && cvalid[ni] && !(own_blk && (cloc[ni] == gi || cloc[ni] == lpos));
-          if (fixed)
-            acc[mi][ni][r] = ok ? fast_exp2(acc[mi][ni][r] * p.acc_scale - M) : 0.f;
-          else
-            acc[mi][ni][r] = ok ? acc[mi][ni][r] * p.acc_scale : kNegInf;
-        }
+              for (int r = 0; r < 4; ++r) {
+                const int tr = rb[mi] + 4 * (lane >> 4) + r;
+                const int gi = r0 + tr, d = tc - tr;
+                const bool drop = (gi >= p.R) | (c0 + tc >= p.R) |
+                                  (own_blk & ((d == D0) | ((d == D1) & (gi < p.n_half)) | ((d == D2) & (gi >= p.n_half))));
+                acc[mi][ni][r] = drop ? kNegInf : acc[mi][ni][r];
+              }
+            }
+          }
       }
+    }
+    if (item < 6) tstamp(41 + 4 * item);  // masks applied
+    const float sc_ = p.acc_scale;
     float2* rowred = reinterpret_cast<float2*>(smem);                // [4 wb][256]
     float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2 wa][256]
-    if (fixed) {
+    if constexpr (fixed) {
+      // Streamed per 16-row block: exponentiate (exp2(-inf) = 0 for the masked elements),
+      // reduce the 4 rows, fold into the column sums; acc[mi] is dead afterwards, which keeps
+      // the epilogue's register footprint at the accumulators'.
+      float csum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
+      for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fast_exp2(acc[mi][ni][r] * sc_ - M);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
           s = row16_sum(s);
-          if ((lane & 15) == 0)
-            rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
+          // every lane of the 16-lane row holds the sum: all write it (no exec-masked block)
+          rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
         }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          csum[ni] += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
+        __builtin_amdgcn_sched_barrier(0);  // keep the blocks streamed (no hoisted exps to spill)
+      }
       if (kind == kTileSymOff) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          float s = 0.f;
-#pragma unroll
-          for (int mi = 0; mi < 8; ++mi)
-            s += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
-          s = xrow_sum(s);
-          if ((lane >> 4) == 0) colred[wa * 256 + cb[ni] + lane] = make_float2(s > 0.f ? M : kNegInf, s);
+          const float s = xrow_sum(csum[ni]);
+          colred[wa * 256 + cb[ni] + (lane & 15)] = make_float2(s > 0.f ? M : kNegInf, s);
         }
       }
     } else {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= sc_;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -614,7 +702,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           float s = fast_exp2(acc[mi][0][r] - ms) + fast_exp2(acc[mi][1][r] - ms) +
                     fast_exp2(acc[mi][2][r] - ms) + fast_exp2(acc[mi][3][r] - ms);
           s = row16_sum(s);
-          if ((lane & 15) == 0) rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(m, s);
+          rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(m, s);
         }
       if (kind == kTileSymOff) {  // column partials = partials of the mirrored rows
 #pragma unroll
@@ -632,11 +720,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
             for (int r = 0; r < 4; ++r) s += fast_exp2(acc[mi][ni][r] - ms);
           s = xrow_sum(s);
-          if ((lane >> 4) == 0) colred[wa * 256 + cb[ni] + lane] = make_float2(m, s);
+          colred[wa * 256 + cb[ni] + (lane & 15)] = make_float2(m, s);
         }
       }
     }
+    if (item < 6) tstamp(42 + 4 * item);  // exponentials and wave reductions done
     __syncthreads();
+    if (item < 6) tstamp(43 + 4 * item);
     if (tid < 256) {
       float2 v = rowred[tid];
       float m = v.x, s = v.y;
@@ -657,7 +747,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
   }  // epilogue scope
   __syncthreads();  // LDS of this item's epilogue is reused by the next item's staging
+  tstamp(9 + 6 * item);
   }  // work items
+  tstamp(2);
+  if constexpr ((ABL & 64) != 0) tval(3, __builtin_amdgcn_s_memrealtime());
 }
 
 // Store-mode coefficient pass: one wave per 128x64 region (wm, wn) of a kept cosine tile
@@ -681,14 +774,18 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const T* src = st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4;
+    for (int np = 0; np < 2; ++np) {
       if constexpr (sizeof(T) == 2) {
-        union { T h[4]; u32x2 u; } pk;
-        pk.u = *reinterpret_cast<const u32x2*>(src);
-        acc[mi][ni] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
+        union { T h[8]; u32x4 u; } pk;
+        pk.u = *reinterpret_cast<const u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8);
+        acc[mi][2 * np] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
+        acc[mi][2 * np + 1] = f32x4{to_f32<T>(pk.h[4]), to_f32<T>(pk.h[5]), to_f32<T>(pk.h[6]), to_f32<T>(pk.h[7])};
       } else {
-        acc[mi][ni] = *reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ni = 2 * np + q;
+          acc[mi][ni] = *reinterpret_cast<const f32x4*>(st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4);
+        }
       }
     }
   coef_epilogue<T, 1>(acc, rb, cb, 128 * wm, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);

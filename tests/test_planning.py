@@ -73,16 +73,24 @@ def test_stream_k_schedule(C, ntiles, nk, cus):
     assert 1 <= G <= cus
     assert s["dp_tiles"] + s["sk_tiles"] == ntiles
     assert s["dp_tiles"] % G == 0  # whole data-parallel rounds
+    # only the remainder of the DP rounds is split
+    assert s["sk_tiles"] == ntiles % cus
     # every stream-K iteration is owned by exactly one block, contiguous ranges
     total = s["sk_tiles"] * nk
     if total:
         ipb = s["ipb"]
-        assert G * ipb >= total and ipb == -(-total // G)  # minimal even split; tail blocks may idle
+        assert G * ipb >= total
         owned = 0
+        pieces = {}
         for b in range(G):
             lo, hi = b * ipb, min((b + 1) * ipb, total)
             owned += max(0, hi - lo)
+            for t in range(lo // nk, (hi - 1) // nk + 1) if hi > lo else []:
+                pieces[t] = pieces.get(t, 0) + 1
         assert owned == total
+        # few contributors per split tile: the last arriver sums at most p_opt + 1 slabs
+        p_opt = max(1, round((0.4 * nk) ** 0.5))
+        assert max(pieces.values()) <= p_opt + 1
     # balance: the busiest block does at most one DP round + ipb steps more than the mean
     mean = ntiles * nk / G
     worst = (s["dp_tiles"] // G) * nk + s["ipb"]
