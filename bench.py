@@ -39,6 +39,13 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.07)
     ap.add_argument("--recompute", action="store_true", help="recompute logits in backward")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--data", default="views", choices=["views", "iid"],
+                    help="views: two noisy views of a shared random-normal basis (positives correlated, "
+                         "as from a SimCLR encoder; what build/bin/ntxent_bench uses); iid: independent "
+                         "random-normal rows")
+    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
+                    help="torch: unfused PyTorch NT-Xent (hipBLASLt GEMM + eager softmax / cross-entropy, "
+                         "the reference's cuBLAS-GEMM + row-kernel design) as an on-device baseline; 1 GPU")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -62,10 +69,22 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     R = 2 * a.batch
-    h = torch.randn(R, a.dim, device=dev, dtype=dt, generator=g).requires_grad_(True)
+    if a.data == "views":  # positive pairs share a random-normal basis: view = basis + 0.5 noise
+        base = torch.randn(a.batch, a.dim, device=dev, generator=g)
+        v1 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
+        v2 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
+        h = torch.cat([v1, v2], 0).to(dt).requires_grad_(True)
+        del base, v1, v2
+    else:
+        h = torch.randn(R, a.dim, device=dev, dtype=dt, generator=g).requires_grad_(True)
+    if a.impl == "torch" and world > 1:
+        raise SystemExit("--impl torch is a single-GPU baseline")
 
     def step():
-        if world > 1:
+        if a.impl == "torch":
+            from ntxent_amd.ops.reference import ntxent_loss as torch_ntxent
+            loss = torch_ntxent(h, a.temperature)
+        elif world > 1:
             loss = dist_ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute,
                                     overlap=not a.no_overlap)
         else:
@@ -113,9 +132,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else value / BASELINE_VALUE,
             "dtype": a.dtype,
-            "data": "synthetic random-normal embeddings",
+            "data": ("synthetic random-normal two-view embeddings (view = shared N(0,1) basis + 0.5 N(0,1))"
+                     if a.data == "views" else "synthetic iid random-normal embeddings"),
             "config": {
-                "model": "NT-Xent loss (SimCLR), fused MFMA fwd+bwd",
+                "model": ("NT-Xent loss (SimCLR), fused MFMA fwd+bwd" if a.impl == "fused"
+                          else "NT-Xent loss (SimCLR), unfused PyTorch baseline (hipBLASLt + eager)"),
                 "global_batch": world * a.batch,
                 "seq_len": None,
                 "batch_per_gpu": a.batch,

@@ -239,24 +239,25 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
   const float tot = block_sum(li, red);
   // Last-block-done final sum (replaces a separate one-thread launch): publish this block's
   // partial, count arrivals; the last block adds all partials in block order (deterministic)
-  // and returns the counter (a fixed slot ahead of the partials) to zero.
+  // and returns the counter (a fixed slot ahead of the partials) to zero. The partial is a
+  // write-through (sc1) 4-byte store and the last block reads the partials with sc1 loads,
+  // so no agent release/acquire is needed (MI355X_MICROARCH.md § visibility, Valid forms
+  // row 1); a release fence here wrote back every dirty L2 line the forward GEMM left behind.
   __shared__ int last;
   int* cnt = reinterpret_cast<int*>(block_loss);  // fixed slot 0: the counter
   float* partial = block_loss + 64;               // per-block partials after it
   if (threadIdx.x == 0) {
-    partial[blockIdx.x] = tot;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(partial + blockIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == (int)gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (last && threadIdx.x < 64) {
     float s = 0.f;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += 64) s += partial[b];
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += 64)
+      s += __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s = wave_sum(s);  // fixed lane assignment and tree: deterministic
     if (threadIdx.x == 0) loss_sum[0] = s * loss_scale;
   }

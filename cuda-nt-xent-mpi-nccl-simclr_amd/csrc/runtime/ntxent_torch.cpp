@@ -17,7 +17,9 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <tuple>
+#include <vector>
 
 #include "ntxent/ntxent.h"
 
@@ -141,6 +143,34 @@ static at::Tensor device_scratch(const at::Tensor& like, size_t bytes, int slot)
   return t;
 }
 
+
+// Placement experiment (NTXENT_SKEW="zq,zqt,sc,cbuf,slabs" in KiB): start the named buffers
+// that many KiB into a slightly larger allocation. The caching allocator hands out large
+// blocks 2 MiB-aligned, so GEMM operands otherwise share their low address bits.
+static at::Tensor skewed_empty(at::IntArrayRef sizes, const at::TensorOptions& o, int slot) {
+  static const std::vector<long> kb = [] {
+    std::vector<long> v(5, 0);
+    if (const char* e = std::getenv("NTXENT_SKEW")) {
+      std::string str(e);
+      size_t pos = 0;
+      for (int i = 0; i < 5 && pos <= str.size(); ++i) {
+        const size_t c = str.find(',', pos);
+        v[i] = std::atol(str.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
+        if (c == std::string::npos) break;
+        pos = c + 1;
+      }
+    }
+    return v;
+  }();
+  const long skew_b = (slot >= 0 && slot < 5) ? kb[slot] * 1024 : 0;
+  if (skew_b == 0) return at::empty(sizes, o);
+  long numel = 1;
+  for (auto d : sizes) numel *= d;
+  const long es = (long)c10::elementSize(c10::typeMetaToScalarType(o.dtype()));
+  const long skew = skew_b / es;
+  return at::empty({numel + skew}, o).narrow(0, skew, numel).view(sizes);
+}
+
 static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
   GemmWorkspace ws;
   ws.num_cus = P.num_cus;
@@ -166,7 +196,7 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::opti
     NTXENT_CHECK(zq.numel() == (long)P.g.rows_pad * P.g.ld_k && zq.scalar_type() == to_scalar(P.bwd()),
                  "zq_out must be [rows_pad, ld_k] in the backward dtype");
   } else {
-    zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())));
+    zq = skewed_empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())), 0);
   }
   at::Tensor zq8;
   if (P.comp == DType::FP8) {
@@ -196,7 +226,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
     NTXENT_CHECK(zqt.numel() == (long)P.g.dim_n * P.g.ld_t && zqt.scalar_type() == zq.scalar_type(),
                  "zqt_out must be [dim_n, ld_t]");
   } else {
-    zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
+    zqt = skewed_empty({P.g.dim_n, P.g.ld_t}, zq.options(), 1);
   }
   launch_transpose(P.bwd(), zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
@@ -211,7 +241,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  if (keep_cos) sc = skewed_empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())), 2);
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -266,7 +296,7 @@ at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Te
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
-  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
+  auto cbuf = skewed_empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options(), 3);
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf));
   return cbuf;
@@ -276,7 +306,7 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
                      const at::Tensor& cpos, const Plan& P) {
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
-  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  auto cbuf = skewed_empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())), 3);
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -289,7 +319,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
   const at::DeviceGuard guard(sc.device());
-  auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
+  auto slabs = skewed_empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat), 4);
   auto ws = gemm_ws(sc, P.n_dz, P);
   launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, slabs.data_ptr<float>(), ws, P.g, cur_stream(sc));
