@@ -13,6 +13,7 @@
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 
 #include <map>
 #include <memory>
@@ -349,7 +350,45 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
-  auto zqt = transpose(pr[0], *P, c10::nullopt);
+  static const bool side_t = [] {
+    const char* e = std::getenv("NTXENT_SIDE_TRANSPOSE");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (!side_t) {
+    auto zqt = transpose(pr[0], *P, c10::nullopt);
+    const bool f8 = comp == DType::FP8;
+    auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
+    auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+    auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+    auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
+    return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
+  }
+  // ZqT (the dZ GEMM's B operand) is first read in the backward: the transpose runs on a side
+  // stream beside the forward GEMM, whose blocks (one per CU, 128 KiB LDS) leave LDS and
+  // memory bandwidth for it, and the current stream joins it after the LSE kernel.
+  const auto dev = h.device().index();
+  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev);
+  // one side stream per device and thread (a fresh pool stream per call paid a new HW queue
+  // on each of the pool's first 32 uses)
+  thread_local std::map<int, c10::hip::HIPStreamMasqueradingAsCUDA> sides;
+  auto sit = sides.find(dev);
+  if (sit == sides.end()) sit = sides.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, dev)).first;
+  const auto side = sit->second;
+  thread_local std::map<int, std::pair<hipEvent_t, hipEvent_t>> evs;
+  auto& ev = evs[dev];
+  if (!ev.first) {
+    // device-scope events: a system-scope release fence per record left ~6-10 us bubbles
+    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev.first, fl));
+    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev.second, fl));
+  }
+  auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
+  NTXENT_HIP_CHECK(hipEventRecord(ev.first, cur.stream()));
+  NTXENT_HIP_CHECK(hipStreamWaitEvent(side.stream(), ev.first, 0));
+  launch_transpose(P->bwd(), pr[0].data_ptr(), zqt.data_ptr(), P->g, side.stream());
+  NTXENT_HIP_CHECK(hipEventRecord(ev.second, side.stream()));
+  c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(pr[0].storage().data_ptr(), side);
+  c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(zqt.storage().data_ptr(), side);
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
@@ -357,6 +396,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
+  NTXENT_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev.second, 0));
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
