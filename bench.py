@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="torch: unfused PyTorch NT-Xent (hipBLASLt GEMM + eager softmax / cross-entropy, "
                          "the reference's cuBLAS-GEMM + row-kernel design) as an on-device baseline; 1 GPU")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -57,10 +60,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if a.gpus != world and world != 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if a.share_gpu else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     import ntxent_amd
     from ntxent_amd.parallel import dist_ntxent_loss
@@ -143,6 +150,7 @@ def main():
                 "dim": a.dim,
                 "temperature": a.temperature,
                 "compute": a.compute,
+                "mfma_dtype": (a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")),
                 "keep_logits": not a.recompute,
                 "parallelism": f"dp{world}",
             },

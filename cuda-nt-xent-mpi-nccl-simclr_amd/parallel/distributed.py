@@ -33,6 +33,41 @@ def _world(group) -> tuple[int, int]:
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+def _is_gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+class _Done:
+    """Completed-work stand-in for the synchronous gloo fallbacks."""
+
+    def wait(self):
+        return True
+
+
+def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group, async_op: bool = False):
+    """``all_gather_into_tensor`` on RCCL (in place: ``inp`` is this rank's slot of ``out``).
+    gloo (the 1-GPU multi-process test backend) gathers into a list and copies."""
+    if not _is_gloo(group):
+        return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+    W = dist.get_world_size(group)
+    parts = list(out.chunk(W, 0))
+    src = inp.detach().to("cpu")  # gloo gathers host tensors only
+    tmp = [torch.empty_like(src) for _ in parts]
+    dist.all_gather(tmp, src, group=group)
+    for p, t in zip(parts, tmp):
+        p.copy_(t.view(p.shape), non_blocking=False)
+    return _Done() if async_op else None
+
+
+def _reduce_scatter_sum(out: torch.Tensor, inp: torch.Tensor, group):
+    if not _is_gloo(group):
+        dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+        return
+    full = inp.clone()  # gloo has no reduce-scatter: all-reduce, keep this rank's slice
+    dist.all_reduce(full, group=group)
+    out.copy_(full.chunk(dist.get_world_size(group), 0)[dist.get_rank(group)])
+
+
 class DistNTXentFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h: torch.Tensor, temperature: float, compute: str, group, keep_logits: bool,
@@ -58,8 +93,8 @@ class DistNTXentFunction(torch.autograd.Function):
         C.transpose(zq, plan, zqt)
         work_z = work_t = None
         if W > 1:
-            work_z = dist.all_gather_into_tensor(fwd_all, fwd, group=group, async_op=True)
-            work_t = dist.all_gather_into_tensor(zqt_all, zqt, group=group, async_op=True)
+            work_z = _all_gather_into(fwd_all, fwd, group, async_op=True)
+            work_t = _all_gather_into(zqt_all, zqt, group, async_op=True)
             if not overlap:
                 work_z.wait()
                 work_z = None
@@ -75,7 +110,7 @@ class DistNTXentFunction(torch.autograd.Function):
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
         if W > 1:
             mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
-            dist.all_gather_into_tensor(lse2_all, mine, group=group)
+            _all_gather_into(lse2_all, mine, group)
             dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
         ctx.plan = plan
         ctx.group = group
@@ -135,7 +170,7 @@ def _reduce_scatter_backward(plan, h, zq, zqt_all, inv, lse2_all, grad_out, grou
     g_cols = (D.t() @ z) * scale                         # d(own terms)/d(every row), column part
     if W > 1:
         mine = torch.empty((R, d), dtype=torch.float32, device=h.device)
-        dist.reduce_scatter_tensor(mine, g_cols.contiguous(), op=dist.ReduceOp.SUM, group=group)
+        _reduce_scatter_sum(mine, g_cols.contiguous(), group)
     else:
         mine = g_cols
     dz = g_rows + mine
