@@ -36,7 +36,7 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 6
 constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
-constexpr int kCoefWaveLds = 64 * (128 * 2 + 16);     // 17 KiB: C^T of one 128x64 region
+constexpr int kCoefWaveLds = 64 * (64 * 2 + 16);      // 9 KiB: C^T of one 64x64 region
 constexpr int kHalfBytes = 128 * kKStepBytes;         // one half-tile of one operand = 16 KiB
 
 struct OperandDesc {
@@ -112,11 +112,11 @@ struct KStream {
 // staged transposed in LDS, then written row-major into slot (mt, nt) with 16-B stores
 // (rows via ds_read_b64_tr_b16) and, for a mirrored tile, into the lower-triangular slot.
 // ------------------------------------------------------------------------------------
-template <typename T, int NW>
-__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb)[8], const int (&cb)[4],
+template <typename T, int NW, int NMI = 8>
+__device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&rb)[NMI], const int (&cb)[4],
                                               int row_base, int col_base, int mt, int nt, int kind,
                                               lds_char* lds, const SimParams& p, int lane) {
-  constexpr int NROWS = NW == 8 ? kTile : 128;
+  constexpr int NROWS = NW == 8 ? kTile : NMI * 16;
   constexpr int NCOLS = NW == 8 ? kTile : 64;
   constexpr int S = NROWS * 2 + 16;  // LDS row stride (bytes) of the C^T staging tile
   constexpr int NT = NW * 64;        // threads in the calling block
@@ -142,7 +142,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[8][4], const int (&rb
   if (kind == kTileSymOff)
     mirror = base + ((long long)(nt - p.row_tile0) * p.col_tiles + p.row_tile0 + mt) * kTileElems;
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
+  for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
     const int row_t0 = rb[mi] + 4 * (lane >> 4);
     const int gi0 = mt * kTile + row_t0;  // 4 consecutive rows
@@ -788,7 +788,14 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
         }
       }
     }
-  coef_epilogue<T, 1>(acc, rb, cb, 128 * wm, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  // two 64-row halves through a 9 KiB staging tile: twice the resident waves of one 128-row
+  // pass (LDS-bound occupancy), more loads in flight on this HBM-bound pass
+  typedef f32x4 half_acc[4][4];
+  typedef int half_rb[4];
+  coef_epilogue<T, 1, 4>(*reinterpret_cast<half_acc*>(&acc[0]), *reinterpret_cast<const half_rb*>(&rb[0]), cb,
+                         128 * wm, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  coef_epilogue<T, 1, 4>(*reinterpret_cast<half_acc*>(&acc[4]), *reinterpret_cast<const half_rb*>(&rb[4]), cb,
+                         128 * wm + 64, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
 }
 
 }  // namespace dev

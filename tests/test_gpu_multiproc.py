@@ -47,7 +47,7 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q):
         loss = dist_ntxent_loss(h, T, compute=compute, keep_logits=keep, overlap=overlap, backward_mode=mode)
         (g,) = torch.autograd.grad(loss, h, torch.tensor(0.7, device=h.device))
         torch.cuda.synchronize()
-        q.put((rank, loss.item(), g.double().cpu()))
+        q.put((rank, loss.item(), g.double().cpu().numpy()))  # by value: no shared-memory fd hand-off
     except Exception as e:  # surface the failure in the parent
         q.put((rank, repr(e), None))
     finally:
@@ -77,6 +77,7 @@ def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode):
         p.join(timeout=60)
     for r, (loss, g) in res.items():
         assert g is not None, f"rank {r} failed: {loss}"
+        res[r] = (loss, torch.from_numpy(g))
     hg = R.global_pair_order([s.float().double() for s in _shards(W, n, dim, seed=11)]).requires_grad_(True)
     lref = R.ntxent_loss(hg, T)
     (gref,) = torch.autograd.grad(lref, hg, torch.tensor(0.7, dtype=torch.float64))
