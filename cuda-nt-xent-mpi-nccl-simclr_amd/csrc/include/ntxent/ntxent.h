@@ -144,12 +144,23 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
 void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g,
                       hipStream_t stream);
 
+// Column-block view for the ring-negatives mode (O(local) memory): the B operand rows of the
+// global column tiles [b_tile0, b_tile0 + row_tiles) live in a one-rank chunk, and the
+// coefficient tiles are written to a compact buffer with c_ld tiles per row starting at
+// global column tile c_tile0. Defaults (c_ld = 0 -> col_tiles) are the all-gather layout.
+struct BlockView {
+  int b_tile0 = 0;
+  int c_ld = 0;
+  int c_tile0 = 0;
+};
+
 // Forward similarity GEMM: tiles of S = zq_local * zq_all^T with the per-row (max, sum)
 // partials epilogue written to part[col_tile][Rpad] (log2 domain). If `sc` is non-null the
 // cosine tile is kept (compute dtype, fragment order) for the backward.
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
-                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
+                      const BlockView& bv = BlockView{});
 
 // Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
@@ -171,7 +182,8 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 // Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `cbuf`.
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
-                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
+                      const BlockView& bv = BlockView{});
 
 // dZ[Rpad][dim_n] = C * Z (fp32), C = the coefficient buffer, zqt_all = [W][dim_n][Rpad]
 // (all-gathered ZqT blocks); tiles from build_dz_tiles(g, 1).

@@ -493,6 +493,9 @@ dev::SimParams base_params(const Geometry& g) {
   p.own0 = g.rank * g.rows_pad;
   p.row_tile0 = g.rank * g.row_tiles;
   p.col_tiles = g.col_tiles;
+  p.b_tile0 = 0;
+  p.c_ld = g.col_tiles;
+  p.c_tile0 = 0;
   p.y_scale = g.inv_temp * dev::kLog2e;
   p.acc_scale = p.y_scale;
   p.cos_scale = 1.0f;
@@ -710,7 +713,7 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream) {
+                      hipStream_t stream, const BlockView& bv) {
   if (ntiles == 0) return;
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
@@ -723,6 +726,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.kbytes = kb;
   p.part = part;
   p.sc = static_cast<char*>(sc);
+  p.b_tile0 = bv.b_tile0;
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
@@ -733,7 +737,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
 
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
-                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, const BlockView& bv) {
   if (ntiles == 0) return;
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
@@ -747,6 +751,9 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   p.cbuf = static_cast<char*>(cbuf);
   p.lse2 = lse2_all;
   p.cpos = cpos;
+  p.b_tile0 = bv.b_tile0;
+  if (bv.c_ld > 0) p.c_ld = bv.c_ld;
+  p.c_tile0 = bv.c_tile0;
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);

@@ -52,6 +52,8 @@ struct SimParams {
   const int4* tiles;
   long long kbytes;      // K bytes handled by one workgroup
   int R, Rpad, n_half, own0, row_tile0, col_tiles;
+  int b_tile0;           // B operand: global column tile of the chunk's first row tile (ring mode)
+  int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
   float acc_scale;       // logit (log2 units) per accumulator unit: y_scale, / kFp8Scale^2 for fp8
   float cos_scale;       // cosine per accumulator unit: 1, or 1 / kFp8Scale^2 for fp8
@@ -137,10 +139,10 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
     lcol[ni] = fixed ? fast_exp2(M - l) : l;
     cvalid[ni] = (col_local0 + col_t) < p.R;
   }
-  T* slot = base + ((long long)mt * p.col_tiles + nt) * kTileElems;
+  T* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
   T* mirror = nullptr;
   if (kind == kTileSymOff)
-    mirror = base + ((long long)(nt - p.row_tile0) * p.col_tiles + p.row_tile0 + mt) * kTileElems;
+    mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   tval(5 + 6 * item, (unsigned long long)nsteps);
   tstamp(6 + 6 * item);
   Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
-  Bb = p.B.base + (long long)nt * p.B.row_tile_stride;
+  Bb = p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride;
   {
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(k0, p.A, nsteps); sa1.init(k0, p.A, nsteps);

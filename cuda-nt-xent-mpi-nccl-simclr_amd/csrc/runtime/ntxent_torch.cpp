@@ -338,6 +338,77 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
   return dh;
 }
 
+// ---- ring-negatives stage ops (O(local) memory; parallel/ring.py) --------------------------
+// `zq_chunk` holds the normalised rows of ONE rank (rows_pad x op_ld): the rank whose global
+// column tiles start at `b_tile0`. `tiles` is an explicit int32 [n, 4] tile list (a subset of
+// the plan's forward tiles).
+static const int4* tile_ptr(const at::Tensor& tiles, int& n) {
+  check_input(tiles, "tiles");
+  NTXENT_CHECK(tiles.dim() == 2 && tiles.size(1) == 4 && tiles.scalar_type() == at::kInt, "tiles must be int32 [n, 4]");
+  n = (int)tiles.size(0);
+  return reinterpret_cast<const int4*>(tiles.data_ptr<int>());
+}
+
+void fwd_stats_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int b_tile0, const at::Tensor& tiles,
+                     const Plan& P, at::Tensor& part) {
+  check_input(zq_local, "zq_local");
+  check_input(zq_chunk, "zq_chunk");
+  check_input(part, "part");
+  NTXENT_CHECK(zq_chunk.numel() == (long)P.g.rows_pad * P.op_ld(), "zq_chunk must be one rank's [rows_pad, ld] rows");
+  NTXENT_CHECK(part.numel() == (long)P.g.col_tiles * P.g.rows_pad * 2 && part.scalar_type() == at::kFloat,
+               "part must be float32 [col_tiles, rows_pad, 2]");
+  int n = 0;
+  const int4* tp = tile_ptr(tiles, n);
+  if (n == 0) return;
+  const at::DeviceGuard guard(zq_local.device());
+  auto ws = gemm_ws(zq_local, n, P);
+  BlockView bv;
+  bv.b_tile0 = b_tile0;
+  launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_chunk.data_ptr(), tp, n,
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), nullptr, ws, P.g, cur_stream(zq_local), bv);
+}
+
+// Coefficient tiles of one column block (recomputed S) into a compact [row_tiles][c_ld] tile
+// buffer whose first column tile is global tile c_tile0.
+at::Tensor coef_gemm_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int b_tile0, const at::Tensor& tiles,
+                           const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P, int c_ld, int c_tile0) {
+  check_input(zq_local, "zq_local");
+  check_input(zq_chunk, "zq_chunk");
+  NTXENT_CHECK(c_ld > 0, "c_ld must be positive");
+  int n = 0;
+  const int4* tp = tile_ptr(tiles, n);
+  const at::DeviceGuard guard(zq_local.device());
+  auto cbuf = at::empty({(long)P.g.row_tiles * c_ld * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  if (n == 0) return cbuf;
+  auto ws = gemm_ws(zq_local, n, P);
+  BlockView bv;
+  bv.b_tile0 = b_tile0;
+  bv.c_ld = c_ld;
+  bv.c_tile0 = c_tile0;
+  launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_chunk.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
+                   cpos.data_ptr<float>(), tp, n, ws, P.g, cur_stream(zq_local), bv);
+  return cbuf;
+}
+
+// dZ contribution of one column block: slabs = C_block [rows_pad x rows_pad] * Z_chunk, with
+// zqt_chunk = that rank's [dim_n, ld_t] transposed rows (a one-block, world-1 geometry).
+at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, const Plan& P) {
+  check_input(cbuf_block, "cbuf_block");
+  check_input(zqt_chunk, "zqt_chunk");
+  NTXENT_CHECK(zqt_chunk.numel() == (long)P.g.dim_n * P.g.ld_t, "zqt_chunk must be [dim_n, ld_t]");
+  NTXENT_CHECK(cbuf_block.numel() == (long)P.g.row_tiles * P.g.row_tiles * kTileElems, "cbuf_block must be row_tiles^2 tiles");
+  const at::DeviceGuard guard(cbuf_block.device());
+  Geometry g1 = P.g;
+  g1.world = 1;
+  g1.rank = 0;
+  g1.col_tiles = g1.row_tiles;
+  auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(cbuf_block, at::kFloat));
+  auto ws = gemm_ws(cbuf_block, P.n_dz, P);
+  launch_dz(P.bwd(), cbuf_block.data_ptr(), zqt_chunk.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
+            P.n_dz, slabs.data_ptr<float>(), ws, g1, cur_stream(cbuf_block));
+  return slabs;
+}
+
 // ---- single-process fused flows ------------------------------------------------------
 // Returns {loss, zq, zqt, inv, lse2, sc, cpos}; `sc` holds the kept cosines (keep_cos) or is
 // undefined.
@@ -544,6 +615,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coef_gemm", &coef_gemm);
   m.def("dz", &dz);
   m.def("norm_bwd", &norm_bwd);
+  m.def("fwd_stats_tiles", &fwd_stats_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
+        py::arg("tiles"), py::arg("plan"), py::arg("part"));
+  m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
+        py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("c_ld"), py::arg("c_tile0"));
+  m.def("dz_block", &dz_block, py::arg("cbuf_block"), py::arg("zqt_chunk"), py::arg("plan"));
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);

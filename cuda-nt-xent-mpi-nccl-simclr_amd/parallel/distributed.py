@@ -181,13 +181,23 @@ def _reduce_scatter_backward(plan, h, zq, zqt_all, inv, lse2_all, grad_out, grou
 
 def dist_ntxent_loss(h_local: torch.Tensor, temperature: float = 0.07, *, group=None, compute: str = "auto",
                      use_mixed_precision: bool = False, keep_logits: bool = True, overlap: bool = True,
-                     backward_mode: str = "symmetric") -> torch.Tensor:
+                     backward_mode: str = "symmetric", negatives: str = "allgather") -> torch.Tensor:
     """Global NT-Xent over the data-parallel group; ``h_local = [h1_r; h2_r]`` on each rank.
 
     backward_mode: ``"symmetric"`` (default: rank-local C = P + P^T - 2 I_pos from the gathered
     LSE, no gradient collective) or ``"reduce_scatter"`` (column gradients reduce-scattered to
     their owners; comparison variant).
+    negatives: ``"allgather"`` (default: every rank's rows gathered, O(R * W R) memory) or
+    ``"ring"`` (rows passed point-to-point around the ring, O(local) memory, see
+    :mod:`parallel.ring`).
     """
+    if negatives not in ("allgather", "ring"):
+        raise ValueError("negatives must be 'allgather' or 'ring'")
+    if negatives == "ring":
+        from .ring import ring_ntxent_loss
+
+        return ring_ntxent_loss(h_local, temperature, group=group, compute=compute,
+                                use_mixed_precision=use_mixed_precision)
     if backward_mode not in ("symmetric", "reduce_scatter"):
         raise ValueError("backward_mode must be 'symmetric' or 'reduce_scatter'")
     if not h_local.is_cuda:

@@ -66,3 +66,46 @@ def emulated_dist_forward_backward(shards: Sequence[torch.Tensor], temperature: 
         slabs = C.dz(cb, zqt_all, P)
         grads.append(C.norm_bwd(slabs, shards[r].contiguous(), invs[r], go, P))
     return loss, grads
+
+
+def emulated_ring_forward_backward(shards: Sequence[torch.Tensor], temperature: float, *, compute: str = "auto",
+                                   grad_out: float = 1.0) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """The ring-negatives stage ops (:mod:`parallel.ring`) for W virtual ranks on one device:
+    every rank r visits the column blocks q = r, r-1, ... with rank q's rows as the chunk."""
+    from .ring import block_tiles
+
+    C = _ext.load()
+    W = len(shards)
+    R, d = shards[0].shape
+    dev = shards[0].device
+    comp = resolve_compute(shards[0].dtype, False, compute)
+    plans = [C.get_plan(R, d, W, r, float(temperature), comp, dev.index) for r in range(W)]
+    Rpad, rt = plans[0].rows_pad, plans[0].row_tiles
+    preps = [C.prep(shards[r].contiguous(), plans[r]) for r in range(W)]
+    zqs = [p[0] for p in preps]
+    lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=dev)
+    loss = torch.zeros((), dtype=torch.float32, device=dev)
+    cposs = []
+    for r in range(W):
+        P = plans[r]
+        tiles = block_tiles(C, P, dev)
+        part = torch.empty((P.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
+        for s in range(W):
+            q = (r - s) % W
+            C.fwd_stats_tiles(zqs[r], zqs[q], q * rt, tiles[q], P, part)
+        cpos = torch.empty((Rpad,), dtype=torch.float32, device=dev)
+        loss = loss + C.lse(part, preps[r][2], lse2_all, cpos, P)
+        cposs.append(cpos)
+    go = torch.tensor([grad_out], dtype=torch.float32, device=dev)
+    grads = []
+    for r in range(W):
+        P = plans[r]
+        tiles = block_tiles(C, P, dev)
+        acc = None
+        for s in range(W):
+            q = (r - s) % W
+            cb = C.coef_gemm_tiles(zqs[r], zqs[q], q * rt, tiles[q], lse2_all, cposs[r], P, rt, q * rt)
+            slabs = C.dz_block(cb, C.transpose(zqs[q], P), P)
+            acc = slabs if acc is None else acc + slabs
+        grads.append(C.norm_bwd(acc, shards[r].contiguous(), preps[r][1], go, P))
+    return loss, grads

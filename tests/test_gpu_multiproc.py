@@ -33,7 +33,7 @@ def _shards(W, n, dim, seed):
     return out
 
 
-def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q):
+def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives="allgather"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -44,7 +44,8 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q):
 
         torch.cuda.set_device(0)
         h = _shards(W, n, dim, seed=11)[rank].float().cuda().requires_grad_(True)
-        loss = dist_ntxent_loss(h, T, compute=compute, keep_logits=keep, overlap=overlap, backward_mode=mode)
+        loss = dist_ntxent_loss(h, T, compute=compute, keep_logits=keep, overlap=overlap, backward_mode=mode,
+                                negatives=negatives)
         (g,) = torch.autograd.grad(loss, h, torch.tensor(0.7, device=h.device))
         torch.cuda.synchronize()
         q.put((rank, loss.item(), g.double().cpu().numpy()))  # by value: no shared-memory fd hand-off
@@ -54,18 +55,20 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("W,n,dim,compute,keep,overlap,mode", [
-    (2, 256, 128, "fp32", True, True, "symmetric"),
-    (2, 300, 96, "fp16", False, True, "symmetric"),
-    (3, 128, 64, "fp16", True, False, "symmetric"),
-    (2, 128, 64, "fp32", True, True, "reduce_scatter"),
+@pytest.mark.parametrize("W,n,dim,compute,keep,overlap,mode,negatives", [
+    (2, 256, 128, "fp32", True, True, "symmetric", "allgather"),
+    (2, 300, 96, "fp16", False, True, "symmetric", "allgather"),
+    (3, 128, 64, "fp16", True, False, "symmetric", "allgather"),
+    (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather"),
+    (2, 256, 128, "fp32", False, True, "symmetric", "ring"),
+    (3, 150, 100, "fp16", False, True, "symmetric", "ring"),
 ])
-def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode):
+def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
     T = 0.1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, W, port, n, dim, T, compute, keep, overlap, mode, q))
+    procs = [ctx.Process(target=_worker, args=(r, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives))
              for r in range(W)]
     for p in procs:
         p.start()

@@ -157,14 +157,46 @@ def build_cpp_targets(objs, force: bool = False, verbose: bool = False):
         list(ex.map(lambda kv: one(*kv), [(n, s) for n, s in targets.items() if s.exists()]))
 
 
+SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-Xarch_host",
+       "-fno-omit-frame-pointer", "-g"]
+
+
+def build_sanitized(verbose: bool = False) -> Path:
+    """Host-only ASan + UBSan build of the C++ tests: build/asan/ntxent_tests. Device code is
+    not instrumented (GPU ASan is not available on the pool); the host runtime, plan building,
+    arena carving and RCCL bootstrap are."""
+    out_dir = BUILD / "asan"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    inc = f"-I{CSRC / 'include'}"
+    objs = []
+    k_obj = out_dir / "ntxent_kernels.o"
+    _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", inc, "-O2", *SAN, "-c",
+          str(CSRC / "kernels" / "ntxent_kernels.hip"), "-o", str(k_obj)], verbose)
+    objs.append(k_obj)
+    for name in RUNTIME_SRCS:
+        obj = out_dir / (Path(name).stem + ".o")
+        _run(_host_cxx() + [inc, "-O1", *SAN, "-c", str(CSRC / "runtime" / name), "-o", str(obj)], verbose)
+        objs.append(obj)
+    t_obj = out_dir / "ntxent_tests.o"
+    _run(_host_cxx() + [inc, "-O1", *SAN, "-c", str(ROOT / "tests" / "cpp" / "ntxent_tests.cpp"), "-o", str(t_obj)],
+         verbose)
+    exe = out_dir / "ntxent_tests"
+    _run([HIPCC, f"--offload-arch={ARCH}", str(t_obj), *map(str, objs), "-o", str(exe), "-fsanitize=address",
+          "-fsanitize=undefined", "-L/opt/rocm/lib", "-lrccl", "-ldl", "-Wl,-rpath,/opt/rocm/lib"], verbose)
+    return exe
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--no-cpp", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="also build build/asan/ntxent_tests (host ASan+UBSan)")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args()
     so = build(force=a.force, cpp_targets=not a.no_cpp, verbose=a.verbose)
     print(f"built {so.relative_to(ROOT)}")
+    if a.asan:
+        print(f"built {build_sanitized(a.verbose).relative_to(ROOT)}")
 
 
 if __name__ == "__main__":
