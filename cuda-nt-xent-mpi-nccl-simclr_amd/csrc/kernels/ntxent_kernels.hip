@@ -156,6 +156,70 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
   }
 }
 
+// Wave-per-pair prologue for d % 8 == 0, d <= 512 * NCH: each lane keeps its NCH chunks of 8
+// features of both rows in registers between the norm and the normalise pass (h is read once)
+// and every reduction is a wave reduction (no LDS, no block barrier); 4 pairs per block.
+template <typename Tin, typename Tc, bool Q8, int NCH>
+__global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
+                                                        float* __restrict__ inv, float* __restrict__ ypos,
+                                                        int R, int d, int dk, int ldk, float y_scale,
+                                                        unsigned char* __restrict__ zq8, int dk8, int ldk8) {
+  const int lane = threadIdx.x & 63;
+  const int n = R >> 1;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;  // whole wave
+  const int pi = i + n;
+  const Tin* hi = h + (long long)i * d;
+  const Tin* hp = h + (long long)pi * d;
+  Tc* zi = zq + (long long)i * ldk;
+  Tc* zp = zq + (long long)pi * ldk;
+  float a[NCH][8], b[NCH][8];
+  float ssi = 0.f, ssp = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 64 + lane) * 8;
+    if (e < d) {
+      load8<Tin>(hi + e, a[c]);
+      load8<Tin>(hp + e, b[c]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[c][j] = 0.f; b[c][j] = 0.f; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ssi += a[c][j] * a[c][j]; ssp += b[c][j] * b[c][j]; }
+  }
+  ssi = wave_sum(ssi);
+  ssp = wave_sum(ssp);
+  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
+  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 64 + lane) * 8;
+    if (e < d) {
+      float qa[8], qb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[c][j] *= ivi; b[c][j] *= ivp; }
+      store8<Tc>(zi + e, a[c], qa);
+      store8<Tc>(zp + e, b[c], qb);
+      if constexpr (Q8) {
+        *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa);
+        *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot += qa[j] * qb[j];
+    }
+  }
+  for (int e = d + lane; e < dk; e += 64) { zi[e] = from_f32<Tc>(0.f); zp[e] = from_f32<Tc>(0.f); }
+  if constexpr (Q8)
+    for (int e = d + lane; e < dk8; e += 64) { zq8[(long long)i * ldk8 + e] = 0; zq8[(long long)pi * ldk8 + e] = 0; }
+  dot = wave_sum(dot);
+  if (lane == 0) {
+    inv[i] = ivi; inv[pi] = ivp;
+    ypos[i] = dot * y_scale; ypos[pi] = dot * y_scale;
+  }
+}
+
 // 64x64 tile transpose with 16-byte global accesses on both sides (rows of Zq in, rows of
 // ZqT out); the LDS tile is padded by 16 B per row.
 template <typename T>
@@ -685,10 +749,30 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
                                       (size_t)(g.rows_pad - g.rows) * g.ld_k8, stream));
   }
   const float ys = g.inv_temp * dev::kLog2e;
+  // wave-per-pair kernel when the rows fit in registers (d <= 2048), else one block per pair
+  const int nch = (g.dim % 8 == 0) ? (g.dim + 511) / 512 : 0;
   dispatch_comp(in, [&](auto tin) {
     using Tin = decltype(tin);
     dispatch_comp(comp, [&](auto tc) {
       using Tc = decltype(tc);
+      if (nch >= 1 && nch <= 4) {
+        const dim3 grid((g.rows / 2 + 3) / 4);
+        auto go = [&](auto nc, auto q8) {
+          constexpr int NC = decltype(nc)::value;
+          constexpr bool Q = decltype(q8)::value;
+          hipLaunchKernelGGL((dev::prep_wave_kernel<Tin, Tc, Q, NC>), grid, dim3(256), 0, stream,
+                             static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim, g.dim_k,
+                             g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8);
+        };
+        auto by_q = [&](auto nc) {
+          if (zq8) go(nc, std::true_type{});
+          else go(nc, std::false_type{});
+        };
+        if (nch == 1) by_q(std::integral_constant<int, 1>{});
+        else if (nch == 2) by_q(std::integral_constant<int, 2>{});
+        else by_q(std::integral_constant<int, 4>{});
+        return;
+      }
       if (zq8)
         hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, true>), dim3(g.rows / 2), dim3(256), 0, stream,
                            static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
