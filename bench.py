@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo)")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture one full fwd+bwd step in a hipGraph (torch.cuda.CUDAGraph) and replay it "
+                         "every step (1 GPU)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -98,6 +101,24 @@ def main():
             loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute)
         (gh,) = torch.autograd.grad(loss, h)
         return loss, gh
+
+    if a.graph:
+        if world > 1:
+            raise SystemExit("--graph is a single-GPU mode")
+        side = torch.cuda.Stream()  # warm-up (plans, scratch, tile lists) outside the capture
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(2, a.warmup)):
+                step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_loss, g_gh = step()
+        eager_step = step
+
+        def step():  # noqa: F811 - every replay runs the complete forward + backward
+            graph.replay()
+            return g_loss, g_gh
 
     for _ in range(a.warmup):
         loss, gh = step()
@@ -153,6 +174,7 @@ def main():
                 "mfma_dtype": (a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")),
                 "keep_logits": not a.recompute,
                 "parallelism": f"dp{world}",
+                "hip_graph": bool(a.graph),
             },
             "loss": lossv,
             "tflops_per_gpu_useful": round(tflops, 1),

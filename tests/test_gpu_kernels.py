@@ -189,3 +189,32 @@ def test_peak_memory_accounting(ext, keep):
     expected = quad + linear + scratch + 2 * rows * dim * 2
     assert peak <= 1.1 * expected, (peak, expected)
     assert peak < 0.5 * 3 * rows * rows * 4, peak  # under half the reference's quadratic fp32 buffers
+
+
+def test_torch_cuda_graph_capture_replay():
+    """The autograd op (forward + backward, side-stream transpose included) captures into a
+    torch.cuda.CUDAGraph (hipGraph) and replays bit-identically: what small batches need, where
+    ~8 kernel launches per step dominate."""
+    import ntxent_amd
+
+    _, h = _inputs(512, 256, torch.bfloat16, seed=3)
+    x = h.clone().requires_grad_(True)
+    # warm up outside the capture: plans, tile lists and scratch are created on first use
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            loss = ntxent_amd.ntxent_loss(x, 0.07)
+            (g,) = torch.autograd.grad(loss, x)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        loss_g = ntxent_amd.ntxent_loss(x, 0.07)
+        (g_g,) = torch.autograd.grad(loss_g, x)
+    eager_loss = ntxent_amd.ntxent_loss(x, 0.07)
+    (eager_g,) = torch.autograd.grad(eager_loss, x)
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert loss_g.item() == eager_loss.item()
+    assert torch.equal(g_g, eager_g)
