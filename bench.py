@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--temperature", type=float, default=0.07)
     ap.add_argument("--recompute", action="store_true", help="recompute logits in backward")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--negatives", default="symmetric", choices=["allgather", "symmetric", "ring"],
+                    help="N>1: symmetric = each rank pair's similarity block computed once (column partials and "
+                         "partner gradient contributions exchanged point to point); allgather = every rank computes "
+                         "its whole row block against the gathered rows; ring = O(local) memory")
     ap.add_argument("--data", default="views", choices=["views", "iid"],
                     help="views: two noisy views of a shared random-normal basis (positives correlated, "
                          "as from a SimCLR encoder; what build/bin/ntxent_bench uses); iid: independent "
@@ -90,16 +94,18 @@ def main():
     if a.impl == "torch" and world > 1:
         raise SystemExit("--impl torch is a single-GPU baseline")
 
+    one = torch.ones((), device=dev)  # d(loss)/d(loss), allocated once outside the timed loop
+
     def step():
         if a.impl == "torch":
             from ntxent_amd.ops.reference import ntxent_loss as torch_ntxent
             loss = torch_ntxent(h, a.temperature)
         elif world > 1:
             loss = dist_ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute,
-                                    overlap=not a.no_overlap)
+                                    overlap=not a.no_overlap, negatives=a.negatives)
         else:
             loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute)
-        (gh,) = torch.autograd.grad(loss, h)
+        (gh,) = torch.autograd.grad(loss, h, grad_outputs=one)
         return loss, gh
 
     if a.graph:
@@ -174,6 +180,7 @@ def main():
                 "mfma_dtype": (a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")),
                 "keep_logits": not a.recompute,
                 "parallelism": f"dp{world}",
+                "negatives": a.negatives if world > 1 else None,
                 "hip_graph": bool(a.graph),
             },
             "loss": lossv,

@@ -96,8 +96,20 @@ struct Geometry {
 
 Geometry make_geometry(int rows, int dim, int world, int rank, float temperature);
 
-// Tile kinds of the forward / coefficient pass.
-enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2 };
+// Tile kinds of the forward / coefficient pass. kTileCross: a tile of another rank's column
+// block that this rank computes for BOTH ranks (symmetric data-parallel mode): its column
+// partials and mirrored coefficients go to per-partner buffers instead of this rank's own.
+enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2, kTileCross = 3 };
+
+// Symmetric data-parallel mode: rank `rank` computes rows [m0, m1) (its row tiles) x columns
+// [k0, k1) (rank q's row tiles) of the similarity block (rank, q); each unordered rank pair's
+// block is computed once across the group (see parallel/symmetric.py for the assignment).
+struct SymJob {
+  int q, m0, m1, k0, k1;
+};
+// Own-block upper triangle (as build_fwd_tiles) followed by the kTileCross tiles of `jobs`,
+// each part in Z-order.
+std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs);
 
 // Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
 // first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered.
@@ -157,10 +169,13 @@ struct BlockView {
 // Forward similarity GEMM: tiles of S = zq_local * zq_all^T with the per-row (max, sum)
 // partials epilogue written to part[col_tile][Rpad] (log2 domain). If `sc` is non-null the
 // cosine tile is kept (compute dtype, fragment order) for the backward.
+// part_x (symmetric mode, kTileCross tiles): column partials for the partner's rows,
+// part_x[(q * row_tiles + mt) * Rpad + (nt % row_tiles) * 256 + c] with q = nt / row_tiles,
+// i.e. rank q's part slots [rank*row_tiles + mt] for its rows.
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                      const BlockView& bv = BlockView{});
+                      const BlockView& bv = BlockView{}, float2* part_x = nullptr);
 
 // Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
@@ -176,8 +191,13 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 // Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
 // `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;
 // upper-triangular tiles of the own-rank block are mirrored; the positive entry is cpos[i].
+// mbuf (symmetric mode): mirrored coefficient tiles of kTileCross tiles, [slots][row_tiles][row_tiles]
+// tiles with slot = (q - rank - 1) mod W (partners rank+1, rank+2, ... in order): tile (mt, nt)
+// lands transposed at mbuf tile (slot, nt % row_tiles, mt), i.e. the block C_{q,rank} that
+// multiplies this rank's rows in rank q's gradient; consecutive slots stack into one tall A.
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
-                 const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream);
+                 const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
+                 void* mbuf = nullptr);
 
 // Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `cbuf`.
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
@@ -189,6 +209,15 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 // (all-gathered ZqT blocks); tiles from build_dz_tiles(g, 1).
 void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
                float* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
+
+// Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
+// columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first
+// K column; `a_panel_tiles` tiles per row panel), B = transposed rows starting at `b` (column
+// offset already applied; rows ld_t apart) in K blocks of `b_kblk_cols` columns, consecutive
+// blocks `b_kblk_stride` elements apart (the rank blocks of ZqT_all). accum: add into `out`.
+void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
+                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, float* out, bool accum,
+                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
 
 // dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
 void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,

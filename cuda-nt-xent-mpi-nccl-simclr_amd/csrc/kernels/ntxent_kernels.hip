@@ -680,6 +680,27 @@ std::vector<int4> build_fwd_tiles(const Geometry& g) {
   return tiles;
 }
 
+std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs) {
+  std::vector<int4> tiles;
+  const int own = g.rank * g.row_tiles;
+  for (int ti = 0; ti < g.row_tiles; ++ti)
+    for (int local = ti; local < g.row_tiles; ++local)
+      tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
+  const size_t n_own = tiles.size();
+  for (const SymJob& j : jobs) {
+    NTXENT_CHECK(j.q >= 0 && j.q < g.world && j.q != g.rank, "sym job: bad partner");
+    NTXENT_CHECK(0 <= j.m0 && j.m0 <= j.m1 && j.m1 <= g.row_tiles && 0 <= j.k0 && j.k0 <= j.k1 &&
+                     j.k1 <= g.row_tiles, "sym job: tile range out of bounds");
+    for (int ti = j.m0; ti < j.m1; ++ti)
+      for (int tj = j.k0; tj < j.k1; ++tj) tiles.push_back(make_int4(ti, j.q * g.row_tiles + tj, kTileCross, 0));
+  }
+  if (std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1) {
+    zorder(tiles, 0, n_own);
+    zorder(tiles, n_own, tiles.size());
+  }
+  return tiles;
+}
+
 int count_own_fwd_tiles(const Geometry& g) { return g.row_tiles * (g.row_tiles + 1) / 2; }
 
 int choose_dz_ksplit(const Geometry& g, int num_cus) {
@@ -797,7 +818,7 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream, const BlockView& bv) {
+                      hipStream_t stream, const BlockView& bv, float2* part_x) {
   if (ntiles == 0) return;
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
@@ -811,6 +832,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.part = part;
   p.sc = static_cast<char*>(sc);
   p.b_tile0 = bv.b_tile0;
+  p.part_x = part_x;
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
@@ -859,12 +881,14 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 }
 
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
-                 const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream) {
+                 const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
+                 void* mbuf) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
   p.tiles = tiles;
   p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
   p.cbuf = static_cast<char*>(cbuf);
+  p.mbuf = static_cast<char*>(mbuf);
   p.lse2 = lse2_all;
   p.cpos = cpos;
   dispatch_comp(comp, [&](auto tc) {
@@ -897,6 +921,39 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.out = slabs;
   p.ldo = g.dim_n;
   p.slab_stride = (long long)g.rows_pad * g.dim_n;
+  const int grid = apply_schedule(p, ntiles, ws, stream);
+  dispatch_comp(comp, [&](auto tc) {
+    using Tc = decltype(tc);
+    launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
+  });
+  NTXENT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
+                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, float* out, bool accum,
+                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
+  if (ntiles == 0 || k_tiles == 0) return;
+  NTXENT_CHECK(k_tiles > 0 && a_panel_tiles >= k_tiles, "dz_view: bad K extent");
+  const long long cs = (long long)dtype_size(comp);
+  dev::SimParams p = base_params(g);
+  p.A.base = static_cast<const char*>(a);
+  p.A.ld = kTile * cs;
+  p.A.row_tile_stride = a_panel_tiles * kTileElems * cs;
+  p.A.kblk = kTile * cs;
+  p.A.kblk_stride = kTileElems * cs;
+  // B: K blocks of transposed rows (rows = embedding dims, ld_t apart), one block per rank
+  NTXENT_CHECK(b_kblk_cols > 0 && b_kblk_cols % kTile == 0, "dz_view: bad B K block");
+  p.B.base = static_cast<const char*>(b);
+  p.B.ld = (long long)g.ld_t * cs;
+  p.B.row_tile_stride = (long long)kTile * g.ld_t * cs;
+  p.B.kblk = b_kblk_cols * cs;
+  p.B.kblk_stride = b_kblk_stride * cs;
+  p.tiles = tiles;
+  p.kbytes = (long long)k_tiles * kTile * cs;
+  p.out = out;
+  p.ldo = g.dim_n;
+  p.slab_stride = (long long)g.rows_pad * g.dim_n;
+  p.accum = accum ? 1 : 0;
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);

@@ -63,9 +63,12 @@ struct SimParams {
   char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
   const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
   const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
+  float2* part_x;        // symmetric mode: column partials of kTileCross tiles (per partner)
+  char* mbuf;            // symmetric mode: mirrored coefficient tiles of kTileCross tiles
   float* out;            // dZ slabs
   long long ldo;         // elements
   long long slab_stride; // elements
+  int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int dbg;               // diagnostic ablations (NTXENT_GEMM_DEBUG; 0 in production)
   unsigned long long* stamps;  // ABL & 32 diagnostic builds: s_memtime per barrier
   // persistent stream-K schedule (see sim_gemm_kernel)
@@ -143,6 +146,11 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   T* mirror = nullptr;
   if (kind == kTileSymOff)
     mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
+  else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
+    const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
+    const int slot = (q - p.row_tile0 / rt - 1 + W) % W;  // partners r+1, r+2, ... -> slots 0, 1, ...
+    mirror = reinterpret_cast<T*>(p.mbuf) + ((long long)(slot * rt + nt % rt) * rt + mt) * kTileElems;
+  }
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
@@ -568,7 +576,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const int col = nt * kTile + cb[ni] + 4 * (lane >> 4);
-        *reinterpret_cast<f32x4*>(out + row * p.ldo + col) = acc[mi][ni];
+        f32x4* o = reinterpret_cast<f32x4*>(out + row * p.ldo + col);
+        *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
       }
     }
   } else if constexpr (MODE == kModeCoef) {
@@ -610,7 +619,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     // exp2 per element feeds both the row and the column partial with a common shift M (no
     // max passes). Smaller tau falls back to per-tile max shifting (2 exps per element).
     const int col_local0 = (nt * kTile) % p.Rpad;
-    const bool own_blk = kind != kTilePlain;
+    const bool own_blk = kind == kTileDiag || kind == kTileSymOff;
+    const bool col_out = kind == kTileSymOff || kind == kTileCross;  // column partials too
     constexpr bool fixed = FX != 0;  // launch_sim_gemm picks FX = p.fixed_shift
     const float M = p.y_scale;
     if (item < 6) tstamp(40 + 4 * item);  // ABL & 64: epilogue phases (cosines stored)
@@ -680,7 +690,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           csum[ni] += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
         __builtin_amdgcn_sched_barrier(0);  // keep the blocks streamed (no hoisted exps to spill)
       }
-      if (kind == kTileSymOff) {
+      if (col_out) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const float s = xrow_sum(csum[ni]);
@@ -706,7 +716,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           s = row16_sum(s);
           rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(m, s);
         }
-      if (kind == kTileSymOff) {  // column partials = partials of the mirrored rows
+      if (col_out) {  // column partials = partials of the mirrored rows
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           float m = kNegInf;
@@ -738,13 +748,18 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         lse_merge(m, s, u.x, u.y);
       }
       p.part[(long long)nt * p.Rpad + mt * kTile + tid] = make_float2(m, s);
-    } else if (kind == kTileSymOff) {
+    } else if (col_out) {
       const int c = tid - 256;
       float2 v = colred[c];
       float m = v.x, s = v.y;
       const float2 u = colred[256 + c];
       lse_merge(m, s, u.x, u.y);
-      p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
+      if (kind == kTileSymOff) {
+        p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
+      } else {  // kTileCross: partner q = nt / rt receives slot (rank, mt) for its rows
+        const int rt = p.Rpad / kTile;
+        p.part_x[(long long)((nt / rt) * rt + mt) * p.Rpad + (nt % rt) * kTile + c] = make_float2(m, s);
+      }
     }
   }
   }  // epilogue scope

@@ -409,6 +409,140 @@ at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, c
   return slabs;
 }
 
+// ---- symmetric data-parallel stage ops (parallel/symmetric.py) -----------------------------
+// Every unordered rank pair's similarity block is computed once across the group: the
+// computing rank keeps row AND column partials (kTileCross tiles), forms both coefficient
+// blocks C_{r,q} and C_{q,r} = C_{r,q}^T from its kept cosines, and produces the partner's
+// gradient contribution C_{q,r} Z_r, which the caller sends to q.
+static std::vector<SymJob> to_jobs(const std::vector<std::tuple<int, int, int, int, int>>& jobs) {
+  std::vector<SymJob> v;
+  for (const auto& j : jobs) v.push_back(SymJob{std::get<0>(j), std::get<1>(j), std::get<2>(j), std::get<3>(j), std::get<4>(j)});
+  return v;
+}
+
+at::Tensor sym_fwd_tiles(const Plan& P, const std::vector<std::tuple<int, int, int, int, int>>& jobs) {
+  return upload_tiles(build_sym_fwd_tiles(P.g, to_jobs(jobs)), P.device);
+}
+
+// Forward tiles `tiles` (own block + kTileCross) over the gathered rows: row partials -> part,
+// column partials of cross tiles -> part_x ([col_tiles, rows_pad, 2], see launch_fwd_stats).
+void fwd_stats_sym(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& tiles, const Plan& P,
+                   at::Tensor& part, at::Tensor& part_x, const c10::optional<at::Tensor>& sc, int first, int count) {
+  check_input(zq_local, "zq_local");
+  check_input(zq_all, "zq_all");
+  check_input(part, "part");
+  check_input(part_x, "part_x");
+  int n = 0;
+  const int4* tp = tile_ptr(tiles, n);
+  NTXENT_CHECK(first >= 0 && count >= 0 && first + count <= n, "tile range out of bounds");
+  const long pn = (long)P.g.col_tiles * P.g.rows_pad * 2;
+  NTXENT_CHECK(part.numel() == pn && part.scalar_type() == at::kFloat, "part must be float32 [col_tiles, rows_pad, 2]");
+  NTXENT_CHECK(part_x.numel() == pn && part_x.scalar_type() == at::kFloat, "part_x must be float32 [col_tiles, rows_pad, 2]");
+  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.op_ld(),
+               "zq_all must be [world*rows_pad, ld] in the forward operand dtype");
+  const bool keep = sc.has_value() && sc->defined();
+  if (keep) NTXENT_CHECK(sc->numel() == (long)n * kTileElems && sc->scalar_type() == to_scalar(P.bwd()),
+                         "sc must hold one tile per entry of `tiles` in the backward dtype");
+  if (count == 0) return;
+  const at::DeviceGuard guard(zq_local.device());
+  auto ws = gemm_ws(zq_local, count, P);
+  char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
+  launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), tp + first, count,
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
+                   reinterpret_cast<float2*>(part_x.data_ptr<float>()));
+}
+
+// Kept cosines of `tiles` -> own coefficient tiles in cbuf ([row_tiles][col_tiles] tiles) and the
+// partners' mirrored blocks in mbuf ([max(1, world/2)][row_tiles][row_tiles] tiles, one slot per partner).
+void coef_sym(const at::Tensor& sbuf, const at::Tensor& tiles, const at::Tensor& lse2_all, const at::Tensor& cpos,
+              const Plan& P, at::Tensor& cbuf, at::Tensor& mbuf) {
+  check_input(sbuf, "sbuf");
+  check_input(cbuf, "cbuf");
+  check_input(mbuf, "mbuf");
+  int n = 0;
+  const int4* tp = tile_ptr(tiles, n);
+  const auto st = to_scalar(P.bwd());
+  NTXENT_CHECK(sbuf.numel() == (long)n * kTileElems && sbuf.scalar_type() == st, "sbuf must hold one tile per entry");
+  NTXENT_CHECK(cbuf.numel() == (long)P.g.row_tiles * P.g.col_tiles * kTileElems && cbuf.scalar_type() == st,
+               "cbuf must be [row_tiles * col_tiles] tiles");
+  // partner slots (q - rank - 1) mod W of the cross tiles run 0 .. W/2 - 1 (parallel/symmetric.py)
+  NTXENT_CHECK(mbuf.numel() == (long)std::max(1, P.g.world / 2) * P.g.row_tiles * P.g.row_tiles * kTileElems &&
+                   mbuf.scalar_type() == st, "mbuf must be [max(1, world/2) * row_tiles * row_tiles] tiles");
+  NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad, "lse2_all must be [world*rows_pad]");
+  if (n == 0) return;
+  const at::DeviceGuard guard(sbuf.device());
+  launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(), tp, n, P.g,
+              cur_stream(sbuf), mbuf.data_ptr());
+}
+
+// out[row tiles m0..m1) (+)= A * B with A = tiles of `abuf` starting at tile index a_tile0 (row
+// panels a_panel_tiles tiles apart; row tile mt at a_tile0 + mt * a_panel_tiles), K = k_tiles * 256
+// columns of B = `bbuf` (ZqT blocks [nblk, dim_n, ld_t], or one [dim_n, ld_t]) starting at block
+// b_block0, column b_col0; a K range longer than one block runs over consecutive whole blocks.
+// `out` is float32 [>= m1 * 256, dim_n] (row tiles may exceed row_tiles: stacked outputs).
+void dz_view(const at::Tensor& abuf, long a_tile0, long a_panel_tiles, const at::Tensor& bbuf, int b_block0, long b_col0,
+             int k_tiles, int m0, int m1, at::Tensor& out, bool accum, const Plan& P) {
+  check_input(abuf, "abuf");
+  check_input(bbuf, "bbuf");
+  check_input(out, "out");
+  const auto st = to_scalar(P.bwd());
+  NTXENT_CHECK(abuf.scalar_type() == st && bbuf.scalar_type() == st, "operands must be in the backward dtype");
+  NTXENT_CHECK(0 <= m0 && m0 <= m1, "bad row tile range");
+  NTXENT_CHECK(k_tiles >= 0 && a_panel_tiles >= k_tiles && a_tile0 >= 0, "bad A view");
+  if (m1 > m0)
+    NTXENT_CHECK(a_tile0 + (long)(m1 - 1) * a_panel_tiles + k_tiles <= abuf.numel() / kTileElems, "A view out of bounds");
+  const long blk = (long)P.g.dim_n * P.g.ld_t;
+  NTXENT_CHECK(bbuf.numel() % blk == 0, "bbuf must be [nblk, dim_n, ld_t]");
+  const long nblk = bbuf.numel() / blk;
+  const long kcols = (long)k_tiles * kTile;
+  long kblk_cols = kcols;
+  if (b_col0 + kcols > P.g.rows_pad) {  // spans whole rank blocks
+    NTXENT_CHECK(b_col0 == 0 && kcols % P.g.rows_pad == 0, "multi-block K ranges must cover whole blocks");
+    kblk_cols = P.g.rows_pad;
+  }
+  const long nspan = (kcols + kblk_cols - 1) / kblk_cols;
+  NTXENT_CHECK(b_block0 >= 0 && b_block0 + nspan <= nblk && b_col0 >= 0, "B view out of bounds");
+  NTXENT_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(1) == P.g.dim_n &&
+                   out.size(0) >= (long)m1 * kTile, "out must be float32 [>= m1*256, dim_n]");
+  if (m1 == m0 || k_tiles == 0) return;
+  const at::DeviceGuard guard(abuf.device());
+  at::Tensor sub;
+  {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int>, at::Tensor> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto& c = cache[{P.device, P.g.dim_n, m0, m1}];
+    if (!c.defined()) {
+      std::vector<int4> v;
+      for (int ti = m0; ti < m1; ++ti)
+        for (int tn = 0; tn < P.g.dim_n / kTile; ++tn) v.push_back(make_int4(ti, tn, 0, 0));
+      c = upload_tiles(v, P.device);
+    }
+    sub = c;
+  }
+  const long cs = (long)dtype_size(P.bwd());
+  const char* a = static_cast<const char*>(abuf.data_ptr()) + a_tile0 * kTileElems * cs;
+  const char* b = static_cast<const char*>(bbuf.data_ptr()) + ((long)b_block0 * blk + b_col0) * cs;
+  auto ws = gemm_ws(abuf, (int)sub.size(0), P);
+  launch_dz_view(P.bwd(), a, a_panel_tiles, b, kblk_cols, blk, k_tiles, reinterpret_cast<const int4*>(sub.data_ptr<int>()),
+                 (int)sub.size(0), out.data_ptr<float>(), accum, ws, P.g, cur_stream(abuf));
+}
+
+// norm_bwd over a stack of partial dZ slabs [nslabs, rows_pad, dim_n] (summed in order).
+at::Tensor norm_bwd_slabs(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
+                          const Plan& P) {
+  check_input(h, "h");
+  check_input(slabs, "slabs");
+  NTXENT_CHECK(slabs.dim() == 3 && slabs.size(1) == P.g.rows_pad && slabs.size(2) == P.g.dim_n &&
+                   slabs.scalar_type() == at::kFloat, "slabs must be float32 [n, rows_pad, dim_n]");
+  const at::DeviceGuard guard(h.device());
+  auto go = grad_out.to(at::kFloat).contiguous();
+  auto dh = at::empty_like(h);
+  launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), (int)slabs.size(0), h.data_ptr(),
+                  inv.data_ptr<float>(), go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
+  return dh;
+}
+
 // ---- single-process fused flows ------------------------------------------------------
 // Returns {loss, zq, zqt, inv, lse2, sc, cpos}; `sc` holds the kept cosines (keep_cos) or is
 // undefined.
@@ -620,6 +754,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
         py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("c_ld"), py::arg("c_tile0"));
   m.def("dz_block", &dz_block, py::arg("cbuf_block"), py::arg("zqt_chunk"), py::arg("plan"));
+  m.def("sym_fwd_tiles", &sym_fwd_tiles, py::arg("plan"), py::arg("jobs"));
+  m.def("fwd_stats_sym", &fwd_stats_sym, py::arg("zq_local"), py::arg("zq_all"), py::arg("tiles"), py::arg("plan"),
+        py::arg("part"), py::arg("part_x"), py::arg("sc"), py::arg("first"), py::arg("count"));
+  m.def("coef_sym", &coef_sym, py::arg("sbuf"), py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
+        py::arg("cbuf"), py::arg("mbuf"));
+  m.def("dz_view", &dz_view, py::arg("abuf"), py::arg("a_tile0"), py::arg("a_panel_tiles"), py::arg("bbuf"),
+        py::arg("b_block0"), py::arg("b_col0"), py::arg("k_tiles"), py::arg("m0"), py::arg("m1"), py::arg("out"),
+        py::arg("accum"), py::arg("plan"));
+  m.def("norm_bwd_slabs", &norm_bwd_slabs, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"),
+        py::arg("plan"));
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);
@@ -663,6 +807,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dz_tile_list", [tiles_to_list](int rows, int dim, int world, int rank) {
     return tiles_to_list(ntxent::build_dz_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), 1));
   }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
+  m.def("sym_fwd_tile_list", [tiles_to_list](int rows, int dim, int world, int rank,
+                                             const std::vector<std::tuple<int, int, int, int, int>>& jobs) {
+    return tiles_to_list(ntxent::build_sym_fwd_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), to_jobs(jobs)));
+  }, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"), py::arg("jobs"));
   m.def("schedule", [](int ntiles, int nk, int num_cus) {
     const auto s = ntxent::make_schedule(ntiles, nk, num_cus);
     py::dict r;

@@ -187,12 +187,19 @@ def dist_ntxent_loss(h_local: torch.Tensor, temperature: float = 0.07, *, group=
     backward_mode: ``"symmetric"`` (default: rank-local C = P + P^T - 2 I_pos from the gathered
     LSE, no gradient collective) or ``"reduce_scatter"`` (column gradients reduce-scattered to
     their owners; comparison variant).
-    negatives: ``"allgather"`` (default: every rank's rows gathered, O(R * W R) memory) or
-    ``"ring"`` (rows passed point-to-point around the ring, O(local) memory, see
-    :mod:`parallel.ring`).
+    negatives: ``"allgather"`` (default: every rank computes its whole row block against the
+    gathered rows), ``"symmetric"`` (each rank pair's similarity block computed once, column
+    partials and partner gradient contributions exchanged point to point, see
+    :mod:`parallel.symmetric`), or ``"ring"`` (rows passed point-to-point around the ring,
+    O(local) memory, see :mod:`parallel.ring`).
     """
-    if negatives not in ("allgather", "ring"):
-        raise ValueError("negatives must be 'allgather' or 'ring'")
+    if negatives not in ("allgather", "ring", "symmetric"):
+        raise ValueError("negatives must be 'allgather', 'symmetric' or 'ring'")
+    if negatives == "symmetric":
+        from .symmetric import sym_ntxent_loss
+
+        return sym_ntxent_loss(h_local, temperature, group=group, compute=compute,
+                               use_mixed_precision=use_mixed_precision)
     if negatives == "ring":
         from .ring import ring_ntxent_loss
 

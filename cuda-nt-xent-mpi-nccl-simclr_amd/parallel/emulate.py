@@ -109,3 +109,67 @@ def emulated_ring_forward_backward(shards: Sequence[torch.Tensor], temperature: 
             acc = slabs if acc is None else acc + slabs
         grads.append(C.norm_bwd(acc, shards[r].contiguous(), preps[r][1], go, P))
     return loss, grads
+
+
+def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: float, *, compute: str = "auto",
+                                  grad_out: float = 1.0) -> Tuple[torch.Tensor, List[torch.Tensor]]:
+    """The symmetric data-parallel stage ops (:mod:`parallel.symmetric`) for W virtual ranks on
+    one device: each rank computes only its assigned cross blocks; the point-to-point
+    exchanges (column partials, partner gradient contributions) become copies."""
+    from .symmetric import sym_coef, sym_grad_slabs, sym_incoming, sym_jobs, sym_own_grad, sym_partner_grads, sym_tiles
+
+    C = _ext.load()
+    W = len(shards)
+    R, d = shards[0].shape
+    dev = shards[0].device
+    comp = resolve_compute(shards[0].dtype, False, compute)
+    plans = [C.get_plan(R, d, W, r, float(temperature), comp, dev.index) for r in range(W)]
+    P0 = plans[0]
+    Rpad, rt = P0.rows_pad, P0.row_tiles
+    f8 = P0.compute_dtype == "fp8"
+    cdt = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[P0.backward_dtype]
+    zq_all = torch.empty((W * Rpad, P0.ld_k), dtype=cdt, device=dev)
+    zqt_all = torch.empty((W, P0.dim_n, P0.ld_t), dtype=cdt, device=dev)
+    zq8_all = torch.empty((W * Rpad, P0.ld_k8), dtype=torch.uint8, device=dev) if f8 else None
+    invs, yposs = [], []
+    for r in range(W):
+        zq = zq_all[r * Rpad:(r + 1) * Rpad]
+        _, inv, ypos, _ = C.prep(shards[r].contiguous(), plans[r], zq, zq8_all[r * Rpad:(r + 1) * Rpad] if f8 else None)
+        C.transpose(zq, plans[r], zqt_all[r])
+        invs.append(inv)
+        yposs.append(ypos)
+    fwd_all = zq8_all if f8 else zq_all
+    parts, parts_x, scs, tiles = [], [], [], []
+    for r in range(W):
+        P = plans[r]
+        t, n = sym_tiles(C, P, dev)
+        part = torch.empty((P.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
+        part_x = torch.empty_like(part)
+        sc = torch.empty((n * 256 * 256,), dtype=cdt, device=dev)
+        C.fwd_stats_sym(fwd_all[r * Rpad:(r + 1) * Rpad], fwd_all, t, P, part, part_x, sc, 0, n)
+        parts.append(part)
+        parts_x.append(part_x)
+        scs.append(sc)
+        tiles.append(t)
+    for r in range(W):  # "send" column partials to their owners
+        for (q, m0, m1, k0, k1) in sym_jobs(W, r, rt):
+            parts[q][r * rt + m0:r * rt + m1, k0 * 256:k1 * 256].copy_(parts_x[r][q * rt + m0:q * rt + m1, k0 * 256:k1 * 256])
+    lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=dev)
+    loss = torch.zeros((), dtype=torch.float32, device=dev)
+    cposs = []
+    for r in range(W):
+        cpos = torch.empty((Rpad,), dtype=torch.float32, device=dev)
+        loss = loss + C.lse(parts[r], yposs[r], lse2_all, cpos, plans[r])
+        cposs.append(cpos)
+    go = torch.tensor([grad_out], dtype=torch.float32, device=dev)
+    bufs = [sym_coef(C, plans[r], W, tiles[r], scs[r], lse2_all, cposs[r]) for r in range(W)]
+    sent = [sym_partner_grads(C, plans[r], W, r, bufs[r][1], zqt_all) for r in range(W)]
+    grads = []
+    for r in range(W):
+        slabs, recvs = sym_grad_slabs(plans[r], W, r, dev)
+        sym_own_grad(C, plans[r], W, r, bufs[r][0], zqt_all, slabs[0])
+        for (buf, _), (p, m0, m1, k0, k1) in zip(recvs, sym_incoming(W, r, rt)):  # "receive"
+            idx = [i for i, (q, *rest) in enumerate(sym_jobs(W, p, rt)) if q == r][0]
+            buf.copy_(sent[p][idx][0])
+        grads.append(C.norm_bwd_slabs(slabs, shards[r].contiguous(), invs[r], go, plans[r]))
+    return loss, grads

@@ -62,6 +62,9 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives
     (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather"),
     (2, 256, 128, "fp32", False, True, "symmetric", "ring"),
     (3, 150, 100, "fp16", False, True, "symmetric", "ring"),
+    (2, 300, 96, "fp16", True, True, "symmetric", "symmetric"),
+    (4, 256, 64, "fp32", True, True, "symmetric", "symmetric"),
+    (3, 384, 80, "fp16", True, True, "symmetric", "symmetric"),
 ])
 def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
     T = 0.1
