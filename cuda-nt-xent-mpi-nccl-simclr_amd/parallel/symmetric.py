@@ -10,10 +10,12 @@ rows) AND the column partials (for q's rows), and the kept cosines give both coe
 blocks C_{r,q} and C_{q,r} = C_{r,q}^T. This is the north star's "reduce-scatter of
 embedding grads on the backward" (BASELINE.json), done point to point over xGMI:
 
-* forward: prep -> all-gather Zq (and ZqT for the backward, asynchronously) while the own
-  upper-triangular tiles run -> the assigned cross tiles -> column partials (2 MiB per block
-  at B=4096) sent point-to-point to their owners -> LSE -> LSE all-gather + loss all-reduce.
-* backward: coefficient pass (own tiles mirrored in place, cross tiles mirrored into a
+* forward: prep -> Zq sent point-to-point to the ranks that compute against it (half of an
+  all-gather's traffic: 4 x 32 MiB per rank at W = 8) while the own upper-triangular tiles
+  run -> the assigned cross tiles -> column partials (2 MiB per block at B=4096) sent to their
+  owners -> LSE -> LSE all-gather + loss all-reduce.
+* backward: partners' ZqT blocks transposed locally; coefficient pass (own tiles mirrored in
+  place, cross tiles mirrored into a
   per-partner buffer) -> the partners' gradient contributions C_{q,r} Z_r (MFMA dZ GEMMs),
   sent point-to-point as soon as they exist (fp32, 64 MiB per block) -> this rank's own
   contributions C_{r,q} Z_q accumulate in the dZ epilogue while the sends run -> received
@@ -36,7 +38,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
-from .distributed import _all_gather_into, _is_gloo, _world
+from .distributed import _all_gather_into, _is_gloo, _world  # noqa: F401
 
 Job = Tuple[int, int, int, int, int]  # (q, m0, m1, k0, k1): my row tiles [m0,m1) x q's row tiles [k0,k1)
 
@@ -142,19 +144,29 @@ class SymNTXentFunction(torch.autograd.Function):
         fwd = fwd_all[r * Rpad:(r + 1) * Rpad]
         _, inv, ypos, _ = C.prep(h, plan, zq, fwd if f8 else None)
         C.transpose(zq, plan, zqt_all[r])
-        work_z = _all_gather_into(fwd_all, fwd, group, async_op=True)
-        work_t = _all_gather_into(zqt_all, zqt_all[r], group, async_op=True)
+        # rows travel only where a block needs them: to the ranks that compute against this rank
+        # (incoming jobs) and from the ranks this one computes against (its jobs) -- half of an
+        # all-gather's traffic; the partners' ZqT blocks are transposed locally in the backward.
+        jobs = sym_jobs(W, r, rt)
+        inc = sym_incoming(W, r, rt)
+        partners = [q for (q, *_) in jobs]
+        sends = [(fwd, p) for (p, *_) in inc]
+        recvs = [(fwd_all[q * Rpad:(q + 1) * Rpad], q) for q in partners]
+        if f8:  # the backward runs on the fp16 rows
+            sends += [(zq, p) for (p, *_) in inc]
+            recvs += [(zq_all[q * Rpad:(q + 1) * Rpad], q) for q in partners]
+        works = _p2p(sends, recvs, group)
         tiles, ntiles = sym_tiles(C, plan, dev)
         n_own = plan.n_own_tiles
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
         C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, n_own)  # overlaps the gather
-        work_z.wait()
+        for w in works:
+            w.wait()
+        del sends, recvs
         C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, n_own, ntiles - n_own)
         # column partials of the cross tiles -> their rows' owners (part slots [r*rt + m0, r*rt + m1))
-        jobs = sym_jobs(W, r, rt)
-        inc = sym_incoming(W, r, rt)
         sends = [(part_x[q * rt + m0:q * rt + m1, k0 * 256:k1 * 256].contiguous(), q) for (q, m0, m1, k0, k1) in jobs]
         recvs = [(torch.empty((m1 - m0, (k1 - k0) * 256, 2), dtype=torch.float32, device=dev), p)
                  for (p, m0, m1, k0, k1) in inc]
@@ -168,23 +180,23 @@ class SymNTXentFunction(torch.autograd.Function):
         mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
         _all_gather_into(lse2_all, mine, group)
         dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
-        ctx.plan, ctx.group, ctx.work_t = plan, group, work_t
+        ctx.plan, ctx.group = plan, group
         ctx.sc = sc
-        ctx.save_for_backward(h, inv, zqt_all, lse2_all, cpos, tiles)
+        ctx.save_for_backward(h, inv, zq_all, zqt_all, lse2_all, cpos, tiles)
         return loss
 
     @staticmethod
     def backward(ctx, grad_out: torch.Tensor):
         C = _ext.load()
-        h, inv, zqt_all, lse2_all, cpos, tiles = ctx.saved_tensors
+        h, inv, zq_all, zqt_all, lse2_all, cpos, tiles = ctx.saved_tensors
         plan, group = ctx.plan, ctx.group
         sc, ctx.sc = ctx.sc, None
         if sc is None:
             raise RuntimeError("symmetric NT-Xent: backward called twice (kept cosines already consumed)")
-        if ctx.work_t is not None:
-            ctx.work_t.wait()
-            ctx.work_t = None
         W, r = _world(group)
+        Rpad = plan.rows_pad
+        for (q, *_) in sym_jobs(W, r, plan.row_tiles):  # partners' B operands of the own dZ GEMMs
+            C.transpose(zq_all[q * Rpad:(q + 1) * Rpad], plan, zqt_all[q])
         dh = sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc, grad_out, group)
         return dh, None, None, None
 
