@@ -686,17 +686,18 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int local = ti; local < g.row_tiles; ++local)
       tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
-  const size_t n_own = tiles.size();
+  const bool z = std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1;
+  if (z) zorder(tiles, 0, tiles.size());
+  // one contiguous Z-ordered segment per job, in job order: a job's tiles can be launched as
+  // soon as its partner's rows have arrived
   for (const SymJob& j : jobs) {
     NTXENT_CHECK(j.q >= 0 && j.q < g.world && j.q != g.rank, "sym job: bad partner");
     NTXENT_CHECK(0 <= j.m0 && j.m0 <= j.m1 && j.m1 <= g.row_tiles && 0 <= j.k0 && j.k0 <= j.k1 &&
                      j.k1 <= g.row_tiles, "sym job: tile range out of bounds");
+    const size_t first = tiles.size();
     for (int ti = j.m0; ti < j.m1; ++ti)
       for (int tj = j.k0; tj < j.k1; ++tj) tiles.push_back(make_int4(ti, j.q * g.row_tiles + tj, kTileCross, 0));
-  }
-  if (std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1) {
-    zorder(tiles, 0, n_own);
-    zorder(tiles, n_own, tiles.size());
+    if (z) zorder(tiles, first, tiles.size());
   }
   return tiles;
 }

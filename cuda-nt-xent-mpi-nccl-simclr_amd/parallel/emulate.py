@@ -116,7 +116,7 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
     """The symmetric data-parallel stage ops (:mod:`parallel.symmetric`) for W virtual ranks on
     one device: each rank computes only its assigned cross blocks; the point-to-point
     exchanges (column partials, partner gradient contributions) become copies."""
-    from .symmetric import sym_coef, sym_grad_slabs, sym_incoming, sym_jobs, sym_own_grad, sym_partner_grads, sym_tiles
+    from .symmetric import sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grad, sym_tiles
 
     C = _ext.load()
     W = len(shards)
@@ -163,13 +163,13 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
         cposs.append(cpos)
     go = torch.tensor([grad_out], dtype=torch.float32, device=dev)
     bufs = [sym_coef(C, plans[r], W, tiles[r], scs[r], lse2_all, cposs[r]) for r in range(W)]
-    sent = [sym_partner_grads(C, plans[r], W, r, bufs[r][1], zqt_all) for r in range(W)]
+    sent = [{job[0]: sym_partner_grad(C, plans[r], W, r, bufs[r][1], zqt_all, job) for job in sym_jobs(W, r, rt)}
+            for r in range(W)]
     grads = []
     for r in range(W):
-        slabs, recvs = sym_grad_slabs(plans[r], W, r, dev)
+        slabs, views = sym_grad_slabs(plans[r], W, r, dev)
         sym_own_grad(C, plans[r], W, r, bufs[r][0], zqt_all, slabs[0])
-        for (buf, _), (p, m0, m1, k0, k1) in zip(recvs, sym_incoming(W, r, rt)):  # "receive"
-            idx = [i for i, (q, *rest) in enumerate(sym_jobs(W, p, rt)) if q == r][0]
-            buf.copy_(sent[p][idx][0])
+        for p, view in views.items():  # "receive"
+            view.copy_(sent[p][r])
         grads.append(C.norm_bwd_slabs(slabs, shards[r].contiguous(), invs[r], go, plans[r]))
     return loss, grads

@@ -74,6 +74,26 @@ def sym_incoming(world: int, rank: int, row_tiles: int) -> List[Job]:
     return out
 
 
+def sym_rounds(world: int, rank: int, row_tiles: int):
+    """Exchange rounds by rank distance d = 1, 2, ...: [(d, job or None, incoming or None)] where
+    job = this rank's block with rank r + d and incoming = rank r - d's block with this rank.
+    Round d is a shift permutation on every rank, so per-round point-to-point batches match."""
+    W, r = world, rank
+    jobs = {(q - r) % W: j for j in sym_jobs(W, r, row_tiles) for q in [j[0]]}
+    inc = {(r - p) % W: j for j in sym_incoming(W, r, row_tiles) for p in [j[0]]}
+    return [(d, jobs.get(d), inc.get(d)) for d in range(1, W // 2 + 1) if d in jobs or d in inc]
+
+
+def sym_job_segments(plan, jobs: List[Job]) -> List[Tuple[int, int]]:
+    """(first, count) of each job's tiles in the symmetric forward tile list."""
+    out, first = [], plan.n_own_tiles
+    for (_, m0, m1, k0, k1) in jobs:
+        n = (m1 - m0) * (k1 - k0)
+        out.append((first, n))
+        first += n
+    return out
+
+
 def sym_work_blocks(world: int, row_tiles: int) -> List[float]:
     """Cross-block tiles per rank in units of full blocks (balance check)."""
     return [sum((m1 - m0) * (k1 - k0) for (_, m0, m1, k0, k1) in sym_jobs(world, r, row_tiles)) / row_tiles ** 2
@@ -144,28 +164,38 @@ class SymNTXentFunction(torch.autograd.Function):
         fwd = fwd_all[r * Rpad:(r + 1) * Rpad]
         _, inv, ypos, _ = C.prep(h, plan, zq, fwd if f8 else None)
         C.transpose(zq, plan, zqt_all[r])
-        # rows travel only where a block needs them: to the ranks that compute against this rank
-        # (incoming jobs) and from the ranks this one computes against (its jobs) -- half of an
-        # all-gather's traffic; the partners' ZqT blocks are transposed locally in the backward.
+        # rows travel only where a block needs them: round d sends this rank's rows to rank r - d
+        # (if it computes against them) and receives rank r + d's (if this rank computes against
+        # them) -- half of an all-gather's traffic, and each partner's cross tiles start as soon
+        # as its rows are in. The partners' ZqT blocks are transposed locally in the backward.
         jobs = sym_jobs(W, r, rt)
         inc = sym_incoming(W, r, rt)
-        partners = [q for (q, *_) in jobs]
-        sends = [(fwd, p) for (p, *_) in inc]
-        recvs = [(fwd_all[q * Rpad:(q + 1) * Rpad], q) for q in partners]
-        if f8:  # the backward runs on the fp16 rows
-            sends += [(zq, p) for (p, *_) in inc]
-            recvs += [(zq_all[q * Rpad:(q + 1) * Rpad], q) for q in partners]
-        works = _p2p(sends, recvs, group)
+        rounds = sym_rounds(W, r, rt)
+        works = []
+        for (dd, job, src) in rounds:
+            sends, recvs = [], []
+            if src is not None:
+                sends.append((fwd, src[0]))
+                if f8:  # the backward runs on the fp16 rows
+                    sends.append((zq, src[0]))
+            if job is not None:
+                q = job[0]
+                recvs.append((fwd_all[q * Rpad:(q + 1) * Rpad], q))
+                if f8:
+                    recvs.append((zq_all[q * Rpad:(q + 1) * Rpad], q))
+            works.append(_p2p(sends, recvs, group))
         tiles, ntiles = sym_tiles(C, plan, dev)
-        n_own = plan.n_own_tiles
+        segs = dict(zip([j[0] for j in jobs], sym_job_segments(plan, jobs)))
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, n_own)  # overlaps the gather
-        for w in works:
-            w.wait()
-        del sends, recvs
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, n_own, ntiles - n_own)
+        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)  # overlaps round 1
+        for (dd, job, src), ws in zip(rounds, works):
+            for w in ws:
+                w.wait()
+            if job is not None:
+                first, count = segs[job[0]]
+                C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
         # column partials of the cross tiles -> their rows' owners (part slots [r*rt + m0, r*rt + m1))
         sends = [(part_x[q * rt + m0:q * rt + m1, k0 * 256:k1 * 256].contiguous(), q) for (q, m0, m1, k0, k1) in jobs]
         recvs = [(torch.empty((m1 - m0, (k1 - k0) * 256, 2), dtype=torch.float32, device=dev), p)
@@ -220,38 +250,31 @@ def sym_coef(C, plan, W, tiles, sc, lse2_all, cpos):
     return cbuf, mbuf
 
 
-def sym_partner_grads(C, plan, W, r, mbuf, zqt_all):
-    """The partners' gradient contributions [(rows, q)]: rows = C_{q,r}[q's tiles k0..k1, my
-    tiles m0..m1) Z_r[m0..m1), fp32 [(k1 - k0) * 256, dim_n], destined for q's rows k0*256...
-    The full blocks are ONE GEMM over the stacked mirror slots (a tall A of slots x row_tiles
-    row panels against Z_r)."""
+def sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job):
+    """One partner's gradient contribution: rows = C_{q,r}[q's tiles k0..k1, my tiles m0..m1)
+    Z_r[m0..m1), fp32 [(k1 - k0) * 256, dim_n], destined for q's rows k0*256... The job's mirror
+    slot is (q - r - 1) mod W."""
     Rpad, rt = plan.rows_pad, plan.row_tiles
-    full, split = _split_jobs(sym_jobs(W, r, rt), rt)
-    sends = []
-    if full:
-        out = torch.empty((len(full) * Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
-        C.dz_view(mbuf, 0, rt, zqt_all, r, 0, rt, 0, len(full) * rt, out, False, plan)
-        sends += [(out[i * Rpad:(i + 1) * Rpad], q) for i, (q, *_) in enumerate(full)]
-    if split is not None:
-        q, m0, m1, k0, k1 = split
-        out = torch.empty((Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
-        C.dz_view(mbuf, len(full) * rt * rt + m0, rt, zqt_all, r, m0 * 256, m1 - m0, k0, k1, out, False, plan)
-        sends.append((out[k0 * 256:k1 * 256], q))
-    return sends
+    q, m0, m1, k0, k1 = job
+    slot = (q - r - 1) % W
+    out = torch.empty((Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
+    C.dz_view(mbuf, slot * rt * rt + m0, rt, zqt_all, r, m0 * 256, m1 - m0, k0, k1, out, False, plan)
+    return out[k0 * 256:k1 * 256]
 
 
 def sym_grad_slabs(plan, W, r, device):
     """[1 + incoming, Rpad, dim_n] fp32: slab 0 = own contributions, slab 1 + i = what incoming
-    job i sends (rows outside its range zeroed), so norm_bwd sums them while reading."""
+    job i (sym_incoming order) sends, rows outside its range zeroed, so norm_bwd sums them all
+    while reading. Returns (slabs, {sender rank: receive view})."""
     inc = sym_incoming(W, r, plan.row_tiles)
     slabs = torch.empty((1 + len(inc), plan.rows_pad, plan.dim_n), dtype=torch.float32, device=device)
-    recvs = []
+    views = {}
     for i, (p, m0, m1, k0, k1) in enumerate(inc):
         sl = slabs[1 + i]
         sl[:k0 * 256].zero_()
         sl[k1 * 256:].zero_()
-        recvs.append((sl[k0 * 256:k1 * 256], p))
-    return slabs, recvs
+        views[p] = sl[k0 * 256:k1 * 256]
+    return slabs, views
 
 
 def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out):
@@ -271,18 +294,25 @@ def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out):
 
 
 def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc, grad_out, group):
-    """Backward of one rank: the partners' contributions are computed first and sent while
-    this rank's own dZ GEMMs run; received contributions land in their own slabs, summed by
-    the normalisation-backward kernel."""
+    """Backward of one rank: round by round, a partner's contribution is computed and sent
+    (while the next one is computed); this rank's own dZ GEMMs run while the transfers finish;
+    received contributions land in their own slabs, summed by the normalisation backward."""
     cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2_all, cpos)
     del sc
-    sends = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
-    slabs, recvs = sym_grad_slabs(plan, W, r, h.device)
-    works = _p2p(sends, recvs, group)
+    slabs, views = sym_grad_slabs(plan, W, r, h.device)
+    works, keep = [], []
+    for (d, job, src) in sym_rounds(W, r, plan.row_tiles):
+        sends = []
+        if job is not None:
+            out = sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job)
+            keep.append(out)
+            sends.append((out, job[0]))
+        recvs = [(views[src[0]], src[0])] if src is not None else []
+        works += _p2p(sends, recvs, group)
     sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
     for w in works:
         w.wait()
-    del sends, cbuf, mbuf
+    del keep, cbuf, mbuf
     return C.norm_bwd_slabs(slabs, h, inv, grad_out.reshape(1), plan)
 
 

@@ -32,7 +32,8 @@ def main():
     a = ap.parse_args()
 
     from ntxent_amd.ops import _ext
-    from ntxent_amd.parallel.symmetric import sym_coef, sym_grad_slabs, sym_own_grad, sym_partner_grads, sym_tiles
+    from ntxent_amd.parallel.symmetric import (sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grad,
+                                               sym_tiles)
 
     C = _ext.load(build_if_missing=False)
     dev = torch.device("cuda", 0)
@@ -86,12 +87,12 @@ def main():
                 C.lse(part, ypos, lse2, cpos, plan)
                 cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2, cpos)
                 del sc
-                sends = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
-                slabs, recvs = sym_grad_slabs(plan, W, r, dev)
+                slabs, views = sym_grad_slabs(plan, W, r, dev)
+                outs = [sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job) for job in sym_jobs(W, r, plan.row_tiles)]
                 sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
-                for (b, _), (o, _) in zip(recvs, sends):  # stands in for the received contributions
-                    if b.shape == o.shape:
-                        b.copy_(o)
+                for v, o in zip(views.values(), outs):  # stands in for the received contributions
+                    if v.shape == o.shape:
+                        v.copy_(o)
                 return C.norm_bwd_slabs(slabs, h, inv, go, plan)
 
             row = {"W": W, "rank": r, "batch": a.batch, "dim": d}
