@@ -51,6 +51,7 @@ class TrainConfig:
     optimizer: str = "lars"          # lars | sgd | adamw
     amp: bool = True                 # bf16 autocast on the GPU
     compute: str = "auto"            # loss compute dtype
+    negatives: str = "symmetric"     # multi-GPU negatives: symmetric | allgather | ring
     sync_bn: bool = True             # global BN statistics (SimCLR)
     num_classes: int = 100
     seed: int = 0
@@ -126,7 +127,8 @@ class SimCLRTrainer:
                 model, device_ids=[device.index] if device.type == "cuda" else None, bucket_cap_mb=64)
         self.opt = build_optimizer(cfg, self.model, self.world)
         self.base_lrs = [g["lr"] for g in self.opt.param_groups]
-        self.loss_fn = NTXentLoss(cfg.temperature, compute=cfg.compute, distributed=self.world > 1)
+        self.loss_fn = NTXentLoss(cfg.temperature, compute=cfg.compute, distributed=self.world > 1,
+                                  negatives=cfg.negatives)
         self.data = SyntheticImages(cfg, device, self.rank)
         self.aug = AugmentConfig(out_size=cfg.image_size)
         self.mem = GPUMemoryTracker() if device.type == "cuda" else None

@@ -95,13 +95,14 @@ def ntxent_loss(h: torch.Tensor, temperature: float = 0.07, *, use_mixed_precisi
 class NTXentLoss(torch.nn.Module):
     """``nn.Module`` front end: ``NTXentLoss(temperature)(z1, z2)`` or ``(h)``.
 
-    With ``distributed=True`` negatives come from the whole data-parallel group (RCCL
-    all-gather over xGMI), see :mod:`parallel.distributed`.
+    With ``distributed=True`` negatives come from the whole data-parallel group over RCCL/xGMI
+    (``negatives``: "allgather", "symmetric" or "ring"), see :mod:`parallel`.
     """
 
     def __init__(self, temperature: float = 0.07, use_mixed_precision: bool = False, compute: str = "auto",
-                 keep_logits: bool = True, distributed: bool = False, group=None):
+                 keep_logits: bool = True, distributed: bool = False, group=None, negatives: str = "allgather"):
         super().__init__()
+        self.negatives = negatives
         self.temperature = float(temperature)
         self.use_mixed_precision = use_mixed_precision
         self.compute = compute
@@ -115,7 +116,8 @@ class NTXentLoss(torch.nn.Module):
             from ..parallel.distributed import dist_ntxent_loss
 
             return dist_ntxent_loss(h, self.temperature, group=self.group, compute=self.compute,
-                                    use_mixed_precision=self.use_mixed_precision, keep_logits=self.keep_logits)
+                                    use_mixed_precision=self.use_mixed_precision, keep_logits=self.keep_logits,
+                                    negatives=self.negatives)
         return ntxent_loss(h, self.temperature, use_mixed_precision=self.use_mixed_precision,
                            compute=self.compute, keep_logits=self.keep_logits)
 
