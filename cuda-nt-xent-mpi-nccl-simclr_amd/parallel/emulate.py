@@ -116,7 +116,7 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
     """The symmetric data-parallel stage ops (:mod:`parallel.symmetric`) for W virtual ranks on
     one device: each rank computes only its assigned cross blocks; the point-to-point
     exchanges (column partials, partner gradient contributions) become copies."""
-    from .symmetric import sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grad, sym_tiles
+    from .symmetric import sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grads, sym_tiles
 
     C = _ext.load()
     W = len(shards)
@@ -163,8 +163,7 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
         cposs.append(cpos)
     go = torch.tensor([grad_out], dtype=torch.float32, device=dev)
     bufs = [sym_coef(C, plans[r], W, tiles[r], scs[r], lse2_all, cposs[r]) for r in range(W)]
-    sent = [{job[0]: sym_partner_grad(C, plans[r], W, r, bufs[r][1], zqt_all, job) for job in sym_jobs(W, r, rt)}
-            for r in range(W)]
+    sent = [sym_partner_grads(C, plans[r], W, r, bufs[r][1], zqt_all) for r in range(W)]
     grads = []
     for r in range(W):
         slabs, views = sym_grad_slabs(plans[r], W, r, dev)

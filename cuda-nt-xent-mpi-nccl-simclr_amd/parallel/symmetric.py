@@ -11,9 +11,10 @@ blocks C_{r,q} and C_{q,r} = C_{r,q}^T. This is the north star's "reduce-scatter
 embedding grads on the backward" (BASELINE.json), done point to point over xGMI:
 
 * forward: prep -> Zq sent point-to-point to the ranks that compute against it (half of an
-  all-gather's traffic: 4 x 32 MiB per rank at W = 8) while the own upper-triangular tiles
-  run -> the assigned cross tiles -> column partials (2 MiB per block at B=4096) sent to their
-  owners -> LSE -> LSE all-gather + loss all-reduce.
+  all-gather's traffic: 4 x 32 MiB per rank at W = 8, one grouped batch so every peer's
+  transfer runs on its own link at once) while the own upper-triangular tiles run -> the
+  assigned cross tiles -> column partials (2 MiB per block at B=4096) sent to their owners ->
+  LSE -> LSE all-gather + loss all-reduce.
 * backward: partners' ZqT blocks transposed locally; coefficient pass (own tiles mirrored in
   place, cross tiles mirrored into a
   per-partner buffer) -> the partners' gradient contributions C_{q,r} Z_r (MFMA dZ GEMMs),
@@ -164,38 +165,29 @@ class SymNTXentFunction(torch.autograd.Function):
         fwd = fwd_all[r * Rpad:(r + 1) * Rpad]
         _, inv, ypos, _ = C.prep(h, plan, zq, fwd if f8 else None)
         C.transpose(zq, plan, zqt_all[r])
-        # rows travel only where a block needs them: round d sends this rank's rows to rank r - d
-        # (if it computes against them) and receives rank r + d's (if this rank computes against
-        # them) -- half of an all-gather's traffic, and each partner's cross tiles start as soon
-        # as its rows are in. The partners' ZqT blocks are transposed locally in the backward.
+        # rows travel only where a block needs them: to the ranks that compute against this
+        # rank's rows and from the ranks this one computes against -- half of an all-gather's
+        # traffic. ONE grouped batch: RCCL runs a group's peers concurrently over their own xGMI
+        # links, while separate batches would serialise on the communicator's stream. The
+        # partners' ZqT blocks are transposed locally in the backward.
         jobs = sym_jobs(W, r, rt)
         inc = sym_incoming(W, r, rt)
-        rounds = sym_rounds(W, r, rt)
-        works = []
-        for (dd, job, src) in rounds:
-            sends, recvs = [], []
-            if src is not None:
-                sends.append((fwd, src[0]))
-                if f8:  # the backward runs on the fp16 rows
-                    sends.append((zq, src[0]))
-            if job is not None:
-                q = job[0]
-                recvs.append((fwd_all[q * Rpad:(q + 1) * Rpad], q))
-                if f8:
-                    recvs.append((zq_all[q * Rpad:(q + 1) * Rpad], q))
-            works.append(_p2p(sends, recvs, group))
+        sends = [(fwd, p) for (p, *_) in inc]
+        recvs = [(fwd_all[q * Rpad:(q + 1) * Rpad], q) for (q, *_) in jobs]
+        if f8:  # the backward runs on the fp16 rows
+            sends += [(zq, p) for (p, *_) in inc]
+            recvs += [(zq_all[q * Rpad:(q + 1) * Rpad], q) for (q, *_) in jobs]
+        works = _p2p(sends, recvs, group)
         tiles, ntiles = sym_tiles(C, plan, dev)
-        segs = dict(zip([j[0] for j in jobs], sym_job_segments(plan, jobs)))
+        n_own = plan.n_own_tiles
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)  # overlaps round 1
-        for (dd, job, src), ws in zip(rounds, works):
-            for w in ws:
-                w.wait()
-            if job is not None:
-                first, count = segs[job[0]]
-                C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
+        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, n_own)  # overlaps the exchange
+        for w in works:
+            w.wait()
+        del sends, recvs
+        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, n_own, ntiles - n_own)
         # column partials of the cross tiles -> their rows' owners (part slots [r*rt + m0, r*rt + m1))
         sends = [(part_x[q * rt + m0:q * rt + m1, k0 * 256:k1 * 256].contiguous(), q) for (q, m0, m1, k0, k1) in jobs]
         recvs = [(torch.empty((m1 - m0, (k1 - k0) * 256, 2), dtype=torch.float32, device=dev), p)
@@ -262,6 +254,23 @@ def sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job):
     return out[k0 * 256:k1 * 256]
 
 
+def sym_partner_grads(C, plan, W, r, mbuf, zqt_all):
+    """All partners' contributions {q: rows}. The full blocks (slots 0 .. nfull-1, partners
+    r+1 .. r+nfull) are ONE GEMM: a tall A of nfull x row_tiles row panels against Z_r."""
+    Rpad, rt = plan.rows_pad, plan.row_tiles
+    jobs = sym_jobs(W, r, rt)
+    full = [j for j in jobs if (j[1], j[2], j[3], j[4]) == (0, rt, 0, rt)]
+    assert jobs[:len(full)] == full
+    out = {}
+    if full:
+        buf = torch.empty((len(full) * Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
+        C.dz_view(mbuf, 0, rt, zqt_all, r, 0, rt, 0, len(full) * rt, buf, False, plan)
+        out.update({q: buf[i * Rpad:(i + 1) * Rpad] for i, (q, *_) in enumerate(full)})
+    for job in jobs[len(full):]:
+        out[job[0]] = sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job)
+    return out
+
+
 def sym_grad_slabs(plan, W, r, device):
     """[1 + incoming, Rpad, dim_n] fp32: slab 0 = own contributions, slab 1 + i = what incoming
     job i (sym_incoming order) sends, rows outside its range zeroed, so norm_bwd sums them all
@@ -294,25 +303,18 @@ def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out):
 
 
 def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc, grad_out, group):
-    """Backward of one rank: round by round, a partner's contribution is computed and sent
-    (while the next one is computed); this rank's own dZ GEMMs run while the transfers finish;
+    """Backward of one rank: the partners' contributions first (one stacked GEMM), sent in one
+    grouped batch (concurrent over the peers' links) while this rank's own dZ GEMMs run;
     received contributions land in their own slabs, summed by the normalisation backward."""
     cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2_all, cpos)
     del sc
+    contrib = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
     slabs, views = sym_grad_slabs(plan, W, r, h.device)
-    works, keep = [], []
-    for (d, job, src) in sym_rounds(W, r, plan.row_tiles):
-        sends = []
-        if job is not None:
-            out = sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job)
-            keep.append(out)
-            sends.append((out, job[0]))
-        recvs = [(views[src[0]], src[0])] if src is not None else []
-        works += _p2p(sends, recvs, group)
+    works = _p2p([(t, q) for q, t in contrib.items()], [(v, p) for p, v in views.items()], group)
     sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
     for w in works:
         w.wait()
-    del keep, cbuf, mbuf
+    del contrib, cbuf, mbuf
     return C.norm_bwd_slabs(slabs, h, inv, grad_out.reshape(1), plan)
 
 

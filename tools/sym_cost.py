@@ -32,8 +32,7 @@ def main():
     a = ap.parse_args()
 
     from ntxent_amd.ops import _ext
-    from ntxent_amd.parallel.symmetric import (sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grad,
-                                               sym_tiles)
+    from ntxent_amd.parallel.symmetric import sym_coef, sym_grad_slabs, sym_own_grad, sym_partner_grads, sym_tiles
 
     C = _ext.load(build_if_missing=False)
     dev = torch.device("cuda", 0)
@@ -88,7 +87,7 @@ def main():
                 cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2, cpos)
                 del sc
                 slabs, views = sym_grad_slabs(plan, W, r, dev)
-                outs = [sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job) for job in sym_jobs(W, r, plan.row_tiles)]
+                outs = list(sym_partner_grads(C, plan, W, r, mbuf, zqt_all).values())
                 sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
                 for v, o in zip(views.values(), outs):  # stands in for the received contributions
                     if v.shape == o.shape:
