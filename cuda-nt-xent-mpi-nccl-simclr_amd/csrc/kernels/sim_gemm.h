@@ -635,7 +635,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       const int r0 = mt * kTile, c0 = col_local0;
       const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
       const bool pad = (r0 + kTile > p.R) || (c0 + kTile > p.R);
-      if (own_blk || pad) {
+      // fragment offsets cb - rb span [-240, 240]: only tiles with some |D| <= 255 hold a self
+      // or positive element (the diagonal band and the two positive bands of the own block)
+      const bool tile_near = own_blk && ((D0 <= 255 && D0 >= -255) || (D1 <= 255 && D1 >= -255) ||
+                                         (D2 <= 255 && D2 >= -255));
+      if (tile_near || pad) {
         // block offsets from the wave index in an SGPR: the tests compile to scalar branches
         const int ws = __builtin_amdgcn_readfirstlane(w);
         const int was = ws >> 2, wbs = ws & 3;
@@ -646,7 +650,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
             const int rbs = 128 * (mi >> 2) + 64 * was + 16 * (mi & 3);
             const int cbs = 128 * (ni >> 1) + 32 * wbs + 16 * (ni & 1);
             const int off = cbs - rbs;
-            const bool near = own_blk && ((off - D0 <= 15 && D0 - off <= 15) || (off - D1 <= 15 && D1 - off <= 15) ||
+            const bool near = tile_near && ((off - D0 <= 15 && D0 - off <= 15) || (off - D1 <= 15 && D1 - off <= 15) ||
                                           (off - D2 <= 15 && D2 - off <= 15));
             const bool edge = (r0 + rbs + 16 > p.R) || (c0 + cbs + 16 > p.R);
             if (near || edge) {
@@ -656,7 +660,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
                 const int tr = rb[mi] + 4 * (lane >> 4) + r;
                 const int gi = r0 + tr, d = tc - tr;
                 const bool drop = (gi >= p.R) | (c0 + tc >= p.R) |
-                                  (own_blk & ((d == D0) | ((d == D1) & (gi < p.n_half)) | ((d == D2) & (gi >= p.n_half))));
+                                  (tile_near & ((d == D0) | ((d == D1) & (gi < p.n_half)) | ((d == D2) & (gi >= p.n_half))));
                 acc[mi][ni][r] = drop ? kNegInf : acc[mi][ni][r];
               }
             }
