@@ -73,3 +73,24 @@ def test_fp8_emulated_ranks():
     ref = torch.nn.functional.cross_entropy(S, R.positive_index(q.shape[0])).item()
     assert abs(loss.item() - ref) < 1e-4 * max(1.0, ref), (loss.item(), ref)
     assert all(torch.isfinite(g).all() for g in grads)
+
+
+@pytest.mark.parametrize("W", [2, 3])
+def test_fp8_emulated_symmetric_ranks(W):
+    """Symmetric data-parallel mode with the fp8 forward: same quantised-oracle loss as the
+    all-gather mode, and the same gradients up to the fp16 backward's rounding."""
+    from ntxent_amd.parallel.emulate import emulated_dist_forward_backward, emulated_sym_forward_backward
+
+    shards = [_rows(300, 128, seed=50 + r) for r in range(W)]
+    dev = [s.float().cuda() for s in shards]
+    loss, grads = emulated_sym_forward_backward(dev, 0.1, compute="fp8")
+    qs = [_quantised(s) for s in shards]
+    q = R.global_pair_order(qs)
+    S = q @ q.t() / 0.1
+    S.fill_diagonal_(float("-inf"))
+    ref = torch.nn.functional.cross_entropy(S, R.positive_index(q.shape[0])).item()
+    assert abs(loss.item() - ref) < 1e-4 * max(1.0, ref), (loss.item(), ref)
+    l2, g2 = emulated_dist_forward_backward(dev, 0.1, compute="fp8")
+    for a, b in zip(grads, g2):
+        rel = ((a.double() - b.double()).norm() / b.double().norm()).item()
+        assert rel < 2e-3, rel
