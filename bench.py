@@ -152,7 +152,8 @@ def main():
         raise SystemExit("non-finite loss or gradient")
     from ntxent_amd.ops.reference import flops_fwd_bwd
 
-    tflops = flops_fwd_bwd(R, world * R, a.dim) / (ms / 1e3) / 1e12
+    tflops = flops_fwd_bwd(R, world * R, a.dim,
+                           symmetric_global=world > 1 and a.negatives == "symmetric") / (ms / 1e3) / 1e12
     if rank == 0:
         out = {
             "metric": "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X",
@@ -184,6 +185,9 @@ def main():
                 "hip_graph": bool(a.graph),
             },
             "loss": lossv,
+            "note": ("global-batch negatives: each rank's rows meet all N*B negatives, so per-GPU similarity "
+                     "work grows linearly with N and the ideal whole-job samples/s is flat in N"
+                     if world > 1 else None),
             "tflops_per_gpu_useful": round(tflops, 1),
         }
         line = json.dumps(out)

@@ -142,11 +142,14 @@ def reference_as_written_forward(z: torch.Tensor, T: float) -> torch.Tensor:
     return -torch.log(torch.diagonal(P)).mean()
 
 
-def flops_fwd_bwd(rows_local: int, rows_global: int, dim: int, symmetric_local: bool = True) -> float:
-    """Useful MFMA FLOPs of one fwd+bwd (store mode): fwd S GEMM (upper-triangular in the
-    own-rank block) + dZ GEMM. Used for TFLOP/s reporting."""
+def flops_fwd_bwd(rows_local: int, rows_global: int, dim: int, symmetric_local: bool = True,
+                  symmetric_global: bool = False) -> float:
+    """MFMA FLOPs of one rank's fwd+bwd (store mode): fwd S GEMM (upper-triangular in the
+    own-rank block; with ``symmetric_global`` each cross-rank block counted once per pair, i.e.
+    half per rank, as parallel/symmetric.py executes it) + dZ GEMM. For TFLOP/s reporting."""
     own = rows_local * rows_local * dim * 2.0
-    fwd = (own / 2 if symmetric_local else own) + rows_local * (rows_global - rows_local) * dim * 2.0
+    remote = rows_local * (rows_global - rows_local) * dim * 2.0
+    fwd = (own / 2 if symmetric_local else own) + (remote / 2 if symmetric_global else remote)
     bwd = rows_local * rows_global * dim * 2.0
     return fwd + bwd
 
