@@ -39,7 +39,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
-from .distributed import _all_gather_into, _is_gloo, _world  # noqa: F401
+from .distributed import _all_gather_into, _is_gloo, _world
 
 Job = Tuple[int, int, int, int, int]  # (q, m0, m1, k0, k1): my row tiles [m0,m1) x q's row tiles [k0,k1)
 
@@ -72,26 +72,6 @@ def sym_incoming(world: int, rank: int, row_tiles: int) -> List[Job]:
         for (q, m0, m1, k0, k1) in sym_jobs(world, p, row_tiles):
             if q == rank:
                 out.append((p, m0, m1, k0, k1))
-    return out
-
-
-def sym_rounds(world: int, rank: int, row_tiles: int):
-    """Exchange rounds by rank distance d = 1, 2, ...: [(d, job or None, incoming or None)] where
-    job = this rank's block with rank r + d and incoming = rank r - d's block with this rank.
-    Round d is a shift permutation on every rank, so per-round point-to-point batches match."""
-    W, r = world, rank
-    jobs = {(q - r) % W: j for j in sym_jobs(W, r, row_tiles) for q in [j[0]]}
-    inc = {(r - p) % W: j for j in sym_incoming(W, r, row_tiles) for p in [j[0]]}
-    return [(d, jobs.get(d), inc.get(d)) for d in range(1, W // 2 + 1) if d in jobs or d in inc]
-
-
-def sym_job_segments(plan, jobs: List[Job]) -> List[Tuple[int, int]]:
-    """(first, count) of each job's tiles in the symmetric forward tile list."""
-    out, first = [], plan.n_own_tiles
-    for (_, m0, m1, k0, k1) in jobs:
-        n = (m1 - m0) * (k1 - k0)
-        out.append((first, n))
-        first += n
     return out
 
 

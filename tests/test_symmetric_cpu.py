@@ -90,25 +90,3 @@ def test_gloo_symmetric_matches_oracle(world, n, dim, tile):
         torch.testing.assert_close(loss, l_ref.detach(), rtol=1e-10, atol=1e-12)
         torch.testing.assert_close(grad[:n], g_ref[r * n:(r + 1) * n], rtol=1e-9, atol=1e-12)
         torch.testing.assert_close(grad[n:], g_ref[N + r * n:N + (r + 1) * n], rtol=1e-9, atol=1e-12)
-
-
-@pytest.mark.parametrize("W", range(2, 10))
-@pytest.mark.parametrize("rt", [1, 2, 5])
-def test_rounds_are_matched_permutations(W, rt):
-    """Round d of every rank sends to r + d's... i.e. rank r's job partner in round d receives
-    from r in ITS round d, so per-round RCCL point-to-point groups pair up on every rank."""
-    from ntxent_amd.parallel.symmetric import sym_rounds
-
-    rounds = {r: {d: (job, src) for (d, job, src) in sym_rounds(W, r, rt)} for r in range(W)}
-    for r in range(W):
-        for d, (job, src) in rounds[r].items():
-            if job is not None:
-                q = job[0]
-                assert (q - r) % W == d
-                assert rounds[q][d][1] is not None and rounds[q][d][1][0] == r
-            if src is not None:
-                p = src[0]
-                assert (r - p) % W == d
-                assert rounds[p][d][0] is not None and rounds[p][d][0][0] == r
-    n_jobs = sum(len(sym_jobs(W, r, rt)) for r in range(W))
-    assert n_jobs == sum(1 for r in range(W) for (_, j, _) in sym_rounds(W, r, rt) if j is not None)
