@@ -215,14 +215,17 @@ void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* ti
 // K column; `a_panel_tiles` tiles per row panel), B = transposed rows starting at `b` (column
 // offset already applied; rows ld_t apart) in K blocks of `b_kblk_cols` columns, consecutive
 // blocks `b_kblk_stride` elements apart (the rank blocks of ZqT_all). accum: add into `out`.
+// out_f16: write `out` as fp16 (rows ldo = dim_n elements apart), no accumulation.
 void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
-                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, float* out, bool accum,
-                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
+                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, void* out, bool accum,
+                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false);
 
 // dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
+// xslabs (optional): nx more fp16 slabs [nx][Rpad][dim_n] added to the sum (received partner
+// contributions of the symmetric data-parallel mode).
 void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,
                      const float* inv, const float* grad_out, void* dh, const Geometry& g,
-                     hipStream_t stream);
+                     hipStream_t stream, const void* xslabs = nullptr, int nx = 0);
 
 // ---- device utilities (reference utils::get_optimal_block_size / check_tensor_core_support
 //      at include/ntxent_kernel.cuh:80-110) ------------------------------------------------

@@ -329,12 +329,15 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
 
 // Vectorised normalisation backward: one 256-thread block per row; each thread owns NCH
 // chunks of 8 contiguous features, kept in registers between the dot pass and the output.
+// xs: nx extra fp16 slabs (received partner contributions, symmetric data-parallel mode) added
+// to the fp32 sum.
 template <typename Tin, int NCH>
 __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int ksplit,
                                                            long long slab_stride, long long ldo,
                                                            const Tin* __restrict__ h, const float* __restrict__ inv,
                                                            const float* __restrict__ grad_out, float alpha_base,
-                                                           Tin* __restrict__ dh, int d) {
+                                                           Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
+                                                           int nx) {
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -352,6 +355,11 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
       for (int k = 1; k < ksplit; ++k) {
         a += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e);
         b += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e + 4);
+      }
+      for (int k = 0; k < nx; ++k) {
+        const half8 x = *reinterpret_cast<const half8*>(xs + k * slab_stride + (long long)i * ldo + e);
+        a += f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+        b += f32x4{(float)x[4], (float)x[5], (float)x[6], (float)x[7]};
       }
       g[c][0] = a[0]; g[c][1] = a[1]; g[c][2] = a[2]; g[c][3] = a[3];
       g[c][4] = b[0]; g[c][5] = b[1]; g[c][6] = b[2]; g[c][7] = b[3];
@@ -379,7 +387,9 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
                                                        long long slab_stride, long long ldo,
                                                        const Tin* __restrict__ h, const float* __restrict__ inv,
                                                        const float* __restrict__ grad_out, float alpha_base,
-                                                       Tin* __restrict__ dh, int d) {
+                                                       Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
+                                                       int nx) {
+  const _Float16* xi = xs + (long long)blockIdx.x * ldo;
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -390,6 +400,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
   for (int e = threadIdx.x; e < d; e += 256) {
     float g = 0.f;
     for (int k = 0; k < ksplit; ++k) g += gi[k * slab_stride + e];
+    for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
     dot += to_f32<Tin>(hi[e]) * iv * g;
   }
   dot = block_sum(dot, red);
@@ -397,6 +408,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
   for (int e = threadIdx.x; e < d; e += 256) {
     float g = 0.f;
     for (int k = 0; k < ksplit; ++k) g += gi[k * slab_stride + e];
+    for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
     const float z = to_f32<Tin>(hi[e]) * iv;
     di[e] = from_f32<Tin>(alpha * iv * (g - z * dot));
   }
@@ -931,8 +943,9 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
 }
 
 void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
-                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, float* out, bool accum,
-                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
+                    long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, void* out, bool accum,
+                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16) {
+  NTXENT_CHECK(!(accum && out_f16), "dz_view: fp16 output cannot accumulate");
   if (ntiles == 0 || k_tiles == 0) return;
   NTXENT_CHECK(k_tiles > 0 && a_panel_tiles >= k_tiles, "dz_view: bad K extent");
   const long long cs = (long long)dtype_size(comp);
@@ -951,10 +964,11 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
   p.B.kblk_stride = b_kblk_stride * cs;
   p.tiles = tiles;
   p.kbytes = (long long)k_tiles * kTile * cs;
-  p.out = out;
+  p.out = static_cast<float*>(out);
   p.ldo = g.dim_n;
   p.slab_stride = (long long)g.rows_pad * g.dim_n;
   p.accum = accum ? 1 : 0;
+  p.out_f16 = out_f16 ? 1 : 0;
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
@@ -964,7 +978,10 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 }
 
 void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h, const float* inv,
-                     const float* grad_out, void* dh, const Geometry& g, hipStream_t stream) {
+                     const float* grad_out, void* dh, const Geometry& g, hipStream_t stream,
+                     const void* xslabs, int nx) {
+  const _Float16* xs = static_cast<const _Float16*>(xslabs);
+  if (xs == nullptr) nx = 0;
   const float alpha_base = (float)(1.0 / ((double)g.global_rows * g.temperature));
   const long long ss = (long long)g.rows_pad * g.dim_n, ldo = g.dim_n;
   const int nch = (g.dim + 2047) / 2048;  // 8-element chunks per thread
@@ -975,16 +992,16 @@ void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h, co
     Tin* dp = static_cast<Tin*>(dh);
     if (vec && nch == 1)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec && nch == 2)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else
       hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss, ldo,
-                         hp, inv, grad_out, alpha_base, dp, g.dim);
+                         hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

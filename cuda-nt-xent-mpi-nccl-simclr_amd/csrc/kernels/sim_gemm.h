@@ -69,6 +69,7 @@ struct SimParams {
   long long ldo;         // elements
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
+  int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
   int dbg;               // diagnostic ablations (NTXENT_GEMM_DEBUG; 0 in production)
   unsigned long long* stamps;  // ABL & 32 diagnostic builds: s_memtime per barrier
   // persistent stream-K schedule (see sim_gemm_kernel)
@@ -576,8 +577,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const int col = nt * kTile + cb[ni] + 4 * (lane >> 4);
-        f32x4* o = reinterpret_cast<f32x4*>(out + row * p.ldo + col);
-        *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
+        if (p.out_f16) {
+          union { _Float16 h[4]; u32x2 u; } pk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
+          *reinterpret_cast<u32x2*>(reinterpret_cast<_Float16*>(out) + row * p.ldo + col) = pk.u;
+        } else {
+          f32x4* o = reinterpret_cast<f32x4*>(out + row * p.ldo + col);
+          *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
+        }
       }
     }
   } else if constexpr (MODE == kModeCoef) {

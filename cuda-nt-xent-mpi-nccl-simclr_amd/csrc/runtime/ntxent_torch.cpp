@@ -502,8 +502,10 @@ void dz_view(const at::Tensor& abuf, long a_tile0, long a_panel_tiles, const at:
   }
   const long nspan = (kcols + kblk_cols - 1) / kblk_cols;
   NTXENT_CHECK(b_block0 >= 0 && b_block0 + nspan <= nblk && b_col0 >= 0, "B view out of bounds");
-  NTXENT_CHECK(out.scalar_type() == at::kFloat && out.dim() == 2 && out.size(1) == P.g.dim_n &&
-                   out.size(0) >= (long)m1 * kTile, "out must be float32 [>= m1*256, dim_n]");
+  const bool out_f16 = out.scalar_type() == at::kHalf;
+  NTXENT_CHECK((out.scalar_type() == at::kFloat || out_f16) && out.dim() == 2 && out.size(1) == P.g.dim_n &&
+                   out.size(0) >= (long)m1 * kTile, "out must be float32 or float16 [>= m1*256, dim_n]");
+  NTXENT_CHECK(!(out_f16 && accum), "fp16 output cannot accumulate");
   if (m1 == m0 || k_tiles == 0) return;
   const at::DeviceGuard guard(abuf.device());
   at::Tensor sub;
@@ -525,21 +527,31 @@ void dz_view(const at::Tensor& abuf, long a_tile0, long a_panel_tiles, const at:
   const char* b = static_cast<const char*>(bbuf.data_ptr()) + ((long)b_block0 * blk + b_col0) * cs;
   auto ws = gemm_ws(abuf, (int)sub.size(0), P);
   launch_dz_view(P.bwd(), a, a_panel_tiles, b, kblk_cols, blk, k_tiles, reinterpret_cast<const int4*>(sub.data_ptr<int>()),
-                 (int)sub.size(0), out.data_ptr<float>(), accum, ws, P.g, cur_stream(abuf));
+                 (int)sub.size(0), out.data_ptr(), accum, ws, P.g, cur_stream(abuf), out_f16);
 }
 
-// norm_bwd over a stack of partial dZ slabs [nslabs, rows_pad, dim_n] (summed in order).
+// norm_bwd over a stack of partial dZ slabs [nslabs, rows_pad, dim_n] fp32, plus optional
+// fp16 slabs `xslabs` [nx, rows_pad, dim_n] (received partner contributions), summed in order.
 at::Tensor norm_bwd_slabs(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
-                          const Plan& P) {
+                          const Plan& P, const c10::optional<at::Tensor>& xslabs) {
   check_input(h, "h");
   check_input(slabs, "slabs");
   NTXENT_CHECK(slabs.dim() == 3 && slabs.size(1) == P.g.rows_pad && slabs.size(2) == P.g.dim_n &&
                    slabs.scalar_type() == at::kFloat, "slabs must be float32 [n, rows_pad, dim_n]");
+  const void* xp = nullptr;
+  int nx = 0;
+  if (xslabs.has_value() && xslabs->defined() && xslabs->numel() > 0) {
+    check_input(*xslabs, "xslabs");
+    NTXENT_CHECK(xslabs->dim() == 3 && xslabs->size(1) == P.g.rows_pad && xslabs->size(2) == P.g.dim_n &&
+                     xslabs->scalar_type() == at::kHalf, "xslabs must be float16 [n, rows_pad, dim_n]");
+    xp = xslabs->data_ptr();
+    nx = (int)xslabs->size(0);
+  }
   const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
   launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), (int)slabs.size(0), h.data_ptr(),
-                  inv.data_ptr<float>(), go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
+                  inv.data_ptr<float>(), go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h), xp, nx);
   return dh;
 }
 
@@ -763,7 +775,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b_block0"), py::arg("b_col0"), py::arg("k_tiles"), py::arg("m0"), py::arg("m1"), py::arg("out"),
         py::arg("accum"), py::arg("plan"));
   m.def("norm_bwd_slabs", &norm_bwd_slabs, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"),
-        py::arg("plan"));
+        py::arg("plan"), py::arg("xslabs") = py::none());
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);

@@ -116,7 +116,8 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
     """The symmetric data-parallel stage ops (:mod:`parallel.symmetric`) for W virtual ranks on
     one device: each rank computes only its assigned cross blocks; the point-to-point
     exchanges (column partials, partner gradient contributions) become copies."""
-    from .symmetric import sym_coef, sym_grad_slabs, sym_jobs, sym_own_grad, sym_partner_grads, sym_tiles
+    from .symmetric import (sym_coef, sym_grad_slabs, sym_jobs, sym_norm_bwd, sym_own_grad, sym_partner_grads,
+                            sym_tiles)
 
     C = _ext.load()
     W = len(shards)
@@ -166,9 +167,9 @@ def emulated_sym_forward_backward(shards: Sequence[torch.Tensor], temperature: f
     sent = [sym_partner_grads(C, plans[r], W, r, bufs[r][1], zqt_all) for r in range(W)]
     grads = []
     for r in range(W):
-        slabs, views = sym_grad_slabs(plans[r], W, r, dev)
-        sym_own_grad(C, plans[r], W, r, bufs[r][0], zqt_all, slabs[0])
+        own, recv, views = sym_grad_slabs(plans[r], W, r, dev)
+        sym_own_grad(C, plans[r], W, r, bufs[r][0], zqt_all, own[0])
         for p, view in views.items():  # "receive"
             view.copy_(sent[p][r])
-        grads.append(C.norm_bwd_slabs(slabs, shards[r].contiguous(), invs[r], go, plans[r]))
+        grads.append(sym_norm_bwd(C, plans[r], own, recv, shards[r].contiguous(), invs[r], go))
     return loss, grads

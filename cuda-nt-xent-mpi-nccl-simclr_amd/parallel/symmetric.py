@@ -18,14 +18,15 @@ embedding grads on the backward" (BASELINE.json), done point to point over xGMI:
 * backward: partners' ZqT blocks transposed locally; coefficient pass (own tiles mirrored in
   place, cross tiles mirrored into a
   per-partner buffer) -> the partners' gradient contributions C_{q,r} Z_r (MFMA dZ GEMMs),
-  sent point-to-point as soon as they exist (fp32, 64 MiB per block) -> this rank's own
+  sent point-to-point as soon as they exist (fp16 for reduced-precision plans: 32 MiB per
+  block) -> this rank's own
   contributions C_{r,q} Z_q accumulate in the dZ epilogue while the sends run -> received
   contributions added -> L2-normalisation backward.
 
 Per GPU at W = 8 (B = 4096/view, d = 2048) the forward similarity work drops from 7.5 to 4
 blocks of 8192 x 8192 x 2048 and the coefficient pass from 7.5 to 4 blocks; the dZ GEMMs stay
-at 8 blocks (half of them produce the partners' contributions). Traffic: 3.5 x 64 MiB of dZ
-contributions per rank, each to a different peer (one xGMI link each), overlapped with the
+at 8 blocks (half of them produce the partners' contributions). Traffic: 3.5 x 32 MiB of fp16
+dZ contributions per rank, each to a different peer (one xGMI link each), overlapped with the
 own-row dZ GEMMs.
 
 The reference has no multi-GPU code at all; the math is SURVEY.md §2.2.
@@ -222,14 +223,21 @@ def sym_coef(C, plan, W, tiles, sc, lse2_all, cpos):
     return cbuf, mbuf
 
 
+def contrib_dtype(plan) -> torch.dtype:
+    """dtype of the partner gradient contributions on the wire: fp16 for the reduced-precision
+    plans (half the xGMI bytes; the contributions are O(1) sums, fp16's 11-bit mantissa is
+    finer than the bf16/fp16 gradient they end up in), fp32 for exact-fp32 plans."""
+    return torch.float32 if plan.backward_dtype == "fp32" else torch.float16
+
+
 def sym_partner_grad(C, plan, W, r, mbuf, zqt_all, job):
     """One partner's gradient contribution: rows = C_{q,r}[q's tiles k0..k1, my tiles m0..m1)
-    Z_r[m0..m1), fp32 [(k1 - k0) * 256, dim_n], destined for q's rows k0*256... The job's mirror
-    slot is (q - r - 1) mod W."""
+    Z_r[m0..m1), [(k1 - k0) * 256, dim_n] in :func:`contrib_dtype`, destined for q's rows
+    k0*256... The job's mirror slot is (q - r - 1) mod W."""
     Rpad, rt = plan.rows_pad, plan.row_tiles
     q, m0, m1, k0, k1 = job
     slot = (q - r - 1) % W
-    out = torch.empty((Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
+    out = torch.empty((Rpad, plan.dim_n), dtype=contrib_dtype(plan), device=mbuf.device)
     C.dz_view(mbuf, slot * rt * rt + m0, rt, zqt_all, r, m0 * 256, m1 - m0, k0, k1, out, False, plan)
     return out[k0 * 256:k1 * 256]
 
@@ -243,7 +251,7 @@ def sym_partner_grads(C, plan, W, r, mbuf, zqt_all):
     assert jobs[:len(full)] == full
     out = {}
     if full:
-        buf = torch.empty((len(full) * Rpad, plan.dim_n), dtype=torch.float32, device=mbuf.device)
+        buf = torch.empty((len(full) * Rpad, plan.dim_n), dtype=contrib_dtype(plan), device=mbuf.device)
         C.dz_view(mbuf, 0, rt, zqt_all, r, 0, rt, 0, len(full) * rt, buf, False, plan)
         out.update({q: buf[i * Rpad:(i + 1) * Rpad] for i, (q, *_) in enumerate(full)})
     for job in jobs[len(full):]:
@@ -252,18 +260,26 @@ def sym_partner_grads(C, plan, W, r, mbuf, zqt_all):
 
 
 def sym_grad_slabs(plan, W, r, device):
-    """[1 + incoming, Rpad, dim_n] fp32: slab 0 = own contributions, slab 1 + i = what incoming
-    job i (sym_incoming order) sends, rows outside its range zeroed, so norm_bwd sums them all
-    while reading. Returns (slabs, {sender rank: receive view})."""
+    """(own, received, views): own = fp32 [1, Rpad, dim_n] for this rank's contributions;
+    received = [incoming, Rpad, dim_n] in :func:`contrib_dtype`, slab i = what incoming job i
+    (sym_incoming order) sends, rows outside its range zeroed; views = {sender: receive view}.
+    The normalisation backward sums them all while reading."""
     inc = sym_incoming(W, r, plan.row_tiles)
-    slabs = torch.empty((1 + len(inc), plan.rows_pad, plan.dim_n), dtype=torch.float32, device=device)
+    own = torch.empty((1, plan.rows_pad, plan.dim_n), dtype=torch.float32, device=device)
+    recv = torch.empty((len(inc), plan.rows_pad, plan.dim_n), dtype=contrib_dtype(plan), device=device)
     views = {}
     for i, (p, m0, m1, k0, k1) in enumerate(inc):
-        sl = slabs[1 + i]
+        sl = recv[i]
         sl[:k0 * 256].zero_()
         sl[k1 * 256:].zero_()
         views[p] = sl[k0 * 256:k1 * 256]
-    return slabs, views
+    return own, recv, views
+
+
+def sym_norm_bwd(C, plan, own, recv, h, inv, grad_out):
+    if recv.dtype == torch.float32:  # exact-fp32 plans: one fp32 stack
+        return C.norm_bwd_slabs(torch.cat([own, recv], 0), h, inv, grad_out.reshape(1), plan)
+    return C.norm_bwd_slabs(own, h, inv, grad_out.reshape(1), plan, recv)
 
 
 def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out):
@@ -289,13 +305,13 @@ def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc
     cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2_all, cpos)
     del sc
     contrib = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
-    slabs, views = sym_grad_slabs(plan, W, r, h.device)
+    own, recv, views = sym_grad_slabs(plan, W, r, h.device)
     works = _p2p([(t, q) for q, t in contrib.items()], [(v, p) for p, v in views.items()], group)
-    sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
+    sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
     for w in works:
         w.wait()
     del contrib, cbuf, mbuf
-    return C.norm_bwd_slabs(slabs, h, inv, grad_out.reshape(1), plan)
+    return sym_norm_bwd(C, plan, own, recv, h, inv, grad_out)
 
 
 def sym_ntxent_loss(h_local: torch.Tensor, temperature: float = 0.07, *, group=None, compute: str = "auto",

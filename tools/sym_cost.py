@@ -32,7 +32,8 @@ def main():
     a = ap.parse_args()
 
     from ntxent_amd.ops import _ext
-    from ntxent_amd.parallel.symmetric import sym_coef, sym_grad_slabs, sym_own_grad, sym_partner_grads, sym_tiles
+    from ntxent_amd.parallel.symmetric import (sym_coef, sym_grad_slabs, sym_norm_bwd, sym_own_grad, sym_partner_grads,
+                                               sym_tiles)
 
     C = _ext.load(build_if_missing=False)
     dev = torch.device("cuda", 0)
@@ -86,13 +87,13 @@ def main():
                 C.lse(part, ypos, lse2, cpos, plan)
                 cbuf, mbuf = sym_coef(C, plan, W, tiles, sc, lse2, cpos)
                 del sc
-                slabs, views = sym_grad_slabs(plan, W, r, dev)
+                own, recv, views = sym_grad_slabs(plan, W, r, dev)
                 outs = list(sym_partner_grads(C, plan, W, r, mbuf, zqt_all).values())
-                sym_own_grad(C, plan, W, r, cbuf, zqt_all, slabs[0])
+                sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
                 for v, o in zip(views.values(), outs):  # stands in for the received contributions
                     if v.shape == o.shape:
                         v.copy_(o)
-                return C.norm_bwd_slabs(slabs, h, inv, go, plan)
+                return sym_norm_bwd(C, plan, own, recv, h, inv, go)
 
             row = {"W": W, "rank": r, "batch": a.batch, "dim": d}
             modes = [("allgather", allgather_step)] + ([("symmetric", symmetric_step)] if W > 1 else [])
