@@ -107,9 +107,10 @@ enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2, kTileCross
 struct SymJob {
   int q, m0, m1, k0, k1;
 };
-// Own-block upper triangle (as build_fwd_tiles) followed by the kTileCross tiles of each job
-// in job order, each segment in Z-order.
-std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs);
+// Own-block upper triangle (as build_fwd_tiles) followed by the kTileCross tiles of `jobs`
+// grouped by chunk of the partners' row tiles (chunk c = tiles [rt*c/n, rt*(c+1)/n)), each
+// segment in Z-order.
+std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs, int nchunks = 1);
 
 // Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
 // first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered.

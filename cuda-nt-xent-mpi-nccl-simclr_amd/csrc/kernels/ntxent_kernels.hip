@@ -692,7 +692,7 @@ std::vector<int4> build_fwd_tiles(const Geometry& g) {
   return tiles;
 }
 
-std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs) {
+std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs, int nchunks) {
   std::vector<int4> tiles;
   const int own = g.rank * g.row_tiles;
   for (int ti = 0; ti < g.row_tiles; ++ti)
@@ -700,15 +700,21 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
       tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
   const bool z = std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1;
   if (z) zorder(tiles, 0, tiles.size());
-  // one contiguous Z-ordered segment per job, in job order: a job's tiles can be launched as
-  // soon as its partner's rows have arrived
   for (const SymJob& j : jobs) {
     NTXENT_CHECK(j.q >= 0 && j.q < g.world && j.q != g.rank, "sym job: bad partner");
     NTXENT_CHECK(0 <= j.m0 && j.m0 <= j.m1 && j.m1 <= g.row_tiles && 0 <= j.k0 && j.k0 <= j.k1 &&
                      j.k1 <= g.row_tiles, "sym job: tile range out of bounds");
+  }
+  NTXENT_CHECK(nchunks >= 1 && nchunks <= g.row_tiles, "sym tiles: bad chunk count");
+  // one contiguous Z-ordered segment per chunk of the partners' row tiles (sym_chunk_bounds):
+  // a chunk's tiles can run as soon as that chunk of every partner's rows has arrived
+  for (int c = 0; c < nchunks; ++c) {
+    const int c0 = (int)((long long)g.row_tiles * c / nchunks), c1 = (int)((long long)g.row_tiles * (c + 1) / nchunks);
     const size_t first = tiles.size();
-    for (int ti = j.m0; ti < j.m1; ++ti)
-      for (int tj = j.k0; tj < j.k1; ++tj) tiles.push_back(make_int4(ti, j.q * g.row_tiles + tj, kTileCross, 0));
+    for (const SymJob& j : jobs)
+      for (int ti = j.m0; ti < j.m1; ++ti)
+        for (int tj = std::max(j.k0, c0); tj < std::min(j.k1, c1); ++tj)
+          tiles.push_back(make_int4(ti, j.q * g.row_tiles + tj, kTileCross, 0));
     if (z) zorder(tiles, first, tiles.size());
   }
   return tiles;

@@ -420,8 +420,8 @@ static std::vector<SymJob> to_jobs(const std::vector<std::tuple<int, int, int, i
   return v;
 }
 
-at::Tensor sym_fwd_tiles(const Plan& P, const std::vector<std::tuple<int, int, int, int, int>>& jobs) {
-  return upload_tiles(build_sym_fwd_tiles(P.g, to_jobs(jobs)), P.device);
+at::Tensor sym_fwd_tiles(const Plan& P, const std::vector<std::tuple<int, int, int, int, int>>& jobs, int nchunks) {
+  return upload_tiles(build_sym_fwd_tiles(P.g, to_jobs(jobs), nchunks), P.device);
 }
 
 // Forward tiles `tiles` (own block + kTileCross) over the gathered rows: row partials -> part,
@@ -766,7 +766,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
         py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("c_ld"), py::arg("c_tile0"));
   m.def("dz_block", &dz_block, py::arg("cbuf_block"), py::arg("zqt_chunk"), py::arg("plan"));
-  m.def("sym_fwd_tiles", &sym_fwd_tiles, py::arg("plan"), py::arg("jobs"));
+  m.def("sym_fwd_tiles", &sym_fwd_tiles, py::arg("plan"), py::arg("jobs"), py::arg("nchunks") = 1);
   m.def("fwd_stats_sym", &fwd_stats_sym, py::arg("zq_local"), py::arg("zq_all"), py::arg("tiles"), py::arg("plan"),
         py::arg("part"), py::arg("part_x"), py::arg("sc"), py::arg("first"), py::arg("count"));
   m.def("coef_sym", &coef_sym, py::arg("sbuf"), py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
@@ -820,9 +820,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return tiles_to_list(ntxent::build_dz_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), 1));
   }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
   m.def("sym_fwd_tile_list", [tiles_to_list](int rows, int dim, int world, int rank,
-                                             const std::vector<std::tuple<int, int, int, int, int>>& jobs) {
-    return tiles_to_list(ntxent::build_sym_fwd_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), to_jobs(jobs)));
-  }, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"), py::arg("jobs"));
+                                             const std::vector<std::tuple<int, int, int, int, int>>& jobs, int nchunks) {
+    return tiles_to_list(
+        ntxent::build_sym_fwd_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), to_jobs(jobs), nchunks));
+  }, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"), py::arg("jobs"), py::arg("nchunks") = 1);
   m.def("schedule", [](int ntiles, int nk, int num_cus) {
     const auto s = ntxent::make_schedule(ntiles, nk, num_cus);
     py::dict r;

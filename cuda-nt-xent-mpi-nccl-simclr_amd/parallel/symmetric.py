@@ -76,6 +76,27 @@ def sym_incoming(world: int, rank: int, row_tiles: int) -> List[Job]:
     return out
 
 
+def sym_chunk_bounds(row_tiles: int, nchunks: int) -> List[Tuple[int, int]]:
+    """Row-tile ranges of the forward exchange chunks (as build_sym_fwd_tiles)."""
+    return [(row_tiles * c // nchunks, row_tiles * (c + 1) // nchunks) for c in range(nchunks)]
+
+
+def sym_num_chunks(row_tiles: int) -> int:
+    """Forward rows travel in up to 4 chunks (8 MiB each at B=4096, d=2048): the cross tiles of
+    chunk c start while chunk c+1 is on the wire."""
+    return max(1, min(4, row_tiles))
+
+
+def sym_chunk_segments(plan, jobs: List[Job], nchunks: int) -> List[Tuple[int, int]]:
+    """(first, count) of each chunk's cross tiles in the symmetric forward tile list."""
+    out, first = [], plan.n_own_tiles
+    for (c0, c1) in sym_chunk_bounds(plan.row_tiles, nchunks):
+        n = sum((m1 - m0) * max(0, min(k1, c1) - max(k0, c0)) for (_, m0, m1, k0, k1) in jobs)
+        out.append((first, n))
+        first += n
+    return out
+
+
 def sym_work_blocks(world: int, row_tiles: int) -> List[float]:
     """Cross-block tiles per rank in units of full blocks (balance check)."""
     return [sum((m1 - m0) * (k1 - k0) for (_, m0, m1, k0, k1) in sym_jobs(world, r, row_tiles)) / row_tiles ** 2
@@ -121,7 +142,7 @@ def sym_tiles(C, plan, device) -> Tuple[torch.Tensor, int]:
     hit = _TILES.get(key)
     if hit is None:
         jobs = sym_jobs(plan.world, plan.rank, plan.row_tiles)
-        t = C.sym_fwd_tiles(plan, jobs)
+        t = C.sym_fwd_tiles(plan, jobs, sym_num_chunks(plan.row_tiles))
         hit = (t, int(t.shape[0]))
         _TILES[key] = hit
     return hit
@@ -147,28 +168,43 @@ class SymNTXentFunction(torch.autograd.Function):
         _, inv, ypos, _ = C.prep(h, plan, zq, fwd if f8 else None)
         C.transpose(zq, plan, zqt_all[r])
         # rows travel only where a block needs them: to the ranks that compute against this
-        # rank's rows and from the ranks this one computes against -- half of an all-gather's
-        # traffic. ONE grouped batch: RCCL runs a group's peers concurrently over their own xGMI
-        # links, while separate batches would serialise on the communicator's stream. The
-        # partners' ZqT blocks are transposed locally in the backward.
+        # rank's rows (only the row tiles they use) and from the ranks this one computes
+        # against -- half of an all-gather's traffic. Chunk c of the rows is one grouped batch
+        # (RCCL runs a group's peers concurrently over their own xGMI links; the chunks follow
+        # each other on the communicator's stream), and the cross tiles of chunk c run while
+        # chunk c+1 is on the wire. The partners' ZqT blocks are transposed locally in the
+        # backward.
         jobs = sym_jobs(W, r, rt)
         inc = sym_incoming(W, r, rt)
-        sends = [(fwd, p) for (p, *_) in inc]
-        recvs = [(fwd_all[q * Rpad:(q + 1) * Rpad], q) for (q, *_) in jobs]
-        if f8:  # the backward runs on the fp16 rows
-            sends += [(zq, p) for (p, *_) in inc]
-            recvs += [(zq_all[q * Rpad:(q + 1) * Rpad], q) for (q, *_) in jobs]
-        works = _p2p(sends, recvs, group)
+        nch = sym_num_chunks(rt)
+        works = []
+        for (c0, c1) in sym_chunk_bounds(rt, nch):
+            sends, recvs = [], []
+            for (p, m0, m1, k0, k1) in inc:  # p uses my row tiles [k0, k1)
+                a0, a1 = max(k0, c0), min(k1, c1)
+                if a0 < a1:
+                    sends.append((fwd[a0 * 256:a1 * 256], p))
+            for (q, m0, m1, k0, k1) in jobs:  # I use q's row tiles [k0, k1)
+                a0, a1 = max(k0, c0), min(k1, c1)
+                if a0 < a1:
+                    recvs.append((fwd_all[q * Rpad + a0 * 256:q * Rpad + a1 * 256], q))
+            works.append(_p2p(sends, recvs, group))
+        if f8:  # the backward runs on the fp16 rows: after the forward chunks
+            works_f16 = _p2p([(zq[k0 * 256:k1 * 256], p) for (p, m0, m1, k0, k1) in inc],
+                             [(zq_all[q * Rpad + k0 * 256:q * Rpad + k1 * 256], q) for (q, m0, m1, k0, k1) in jobs], group)
+        else:
+            works_f16 = []
         tiles, ntiles = sym_tiles(C, plan, dev)
-        n_own = plan.n_own_tiles
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, n_own)  # overlaps the exchange
-        for w in works:
+        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)  # overlaps chunk 0
+        for ws, (first, count) in zip(works, sym_chunk_segments(plan, jobs, nch)):
+            for w in ws:
+                w.wait()
+            C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
+        for w in works_f16:
             w.wait()
-        del sends, recvs
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, n_own, ntiles - n_own)
         # column partials of the cross tiles -> their rows' owners (part slots [r*rt + m0, r*rt + m1))
         sends = [(part_x[q * rt + m0:q * rt + m1, k0 * 256:k1 * 256].contiguous(), q) for (q, m0, m1, k0, k1) in jobs]
         recvs = [(torch.empty((m1 - m0, (k1 - k0) * 256, 2), dtype=torch.float32, device=dev), p)

@@ -65,6 +65,7 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives
     (2, 300, 96, "fp16", True, True, "symmetric", "symmetric"),
     (4, 256, 64, "fp32", True, True, "symmetric", "symmetric"),
     (3, 384, 80, "fp16", True, True, "symmetric", "symmetric"),
+    (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric"),  # 16 row tiles: 4 exchange chunks
 ])
 def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
     T = 0.1
