@@ -32,8 +32,13 @@ struct EngineConfig {
   int dim = 0;
   float temperature = 0.07f;
   DType input = DType::BF16;  // dtype of h / dh
-  DType compute = DType::F16; // MFMA operand dtype (fp32 = exact path; FP8 = e4m3 forward GEMM,
-                              // fp16 backward, cosines always kept)
+  // MFMA operand dtype (fp32 = exact path; FP8 = e4m3 forward GEMM, fp16 backward, cosines
+  // always kept). Default: fp16, or bf16 in a CMake -DUSE_FP16=OFF build.
+#ifdef NTXENT_DEFAULT_COMPUTE_BF16
+  DType compute = DType::BF16;
+#else
+  DType compute = DType::F16;
+#endif
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
   bool check_finite = false;  // loss() throws on a non-finite loss
   int device = -1;            // -1: current device

@@ -30,6 +30,9 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   world_ = comm ? comm->world() : 1;
   g_ = make_geometry(cfg.rows, cfg.dim, world_, rank_, cfg.temperature);
   f8_ = cfg.compute == DType::FP8;
+#ifdef NTXENT_NO_FP8
+  if (f8_) throw std::runtime_error("ntxent::Engine: fp8 compute requested but this build has ENABLE_FP8=OFF");
+#endif
   if (f8_) cfg_.keep_cos = true;  // fp8: the fp16 backward uses the forward's own cosines
   bwd_ = backward_dtype(cfg.compute);
   cs_ = dtype_size(bwd_);

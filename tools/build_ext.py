@@ -42,6 +42,10 @@ def _feature_defines():
     d = []
     if os.environ.get("NTXENT_ENABLE_PROFILING", "0") == "1":
         d.append("-DNTXENT_PROFILING_DEFAULT=1")
+    if os.environ.get("NTXENT_USE_FP16", "1") == "0":  # CMake USE_FP16=OFF
+        d.append("-DNTXENT_DEFAULT_COMPUTE_BF16=1")
+    if os.environ.get("NTXENT_ENABLE_FP8", "1") == "0":  # CMake ENABLE_FP8=OFF
+        d.append("-DNTXENT_NO_FP8=1")
     return d
 
 
