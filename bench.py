@@ -2,11 +2,21 @@
 """Headline benchmark: NT-Xent fwd+bwd samples/s, B=4096 per view per GPU, d=2048, bf16.
 
 BASELINE.json metric: "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X".
-One rank per GPU (torchrun); for N>1 negatives are gathered over RCCL/xGMI, so each GPU's
-similarity work grows with N (global batch = N * 4096 pairs) while its own batch is fixed
-(weak scaling). A "sample" is one positive pair. Inputs are synthetic random-normal
-embeddings (no dataset); the timed region is the complete loss forward + backward
-(gradient w.r.t. the embeddings) of every step.
+One rank per GPU; for N>1 negatives are exchanged over RCCL/xGMI, so each GPU's similarity
+work grows with N (global batch = N * 4096 pairs) while its own batch is fixed (weak
+scaling). A "sample" is one positive pair. Inputs are synthetic random-normal embeddings (no
+dataset); the timed region is the complete loss forward + backward (gradient w.r.t. the
+embeddings) of every step.
+
+Launch modes (the reference only links MPI/NCCL in CMake, /root/reference/CMakeLists.txt:13-14,
+41-47; here the ranks are real processes over RCCL):
+  * ``python bench.py --gpus N``: with no WORLD_SIZE in the environment and N > 1 this process
+    is a LAUNCHER. It never touches the GPU; it starts N rank processes of this script
+    (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1/MASTER_PORT set), relays rank 0's single
+    JSON line, and exits non-zero if any rank fails or the job exceeds ``--timeout``.
+  * ``torchrun --nproc-per-node N bench.py --gpus N``: each process is a rank already.
+A rank whose WORLD_SIZE disagrees with ``--gpus`` exits with an error (never silently runs
+fewer GPUs than asked).
 
   python bench.py [--gpus N --steps K --warmup W --batch 4096 --dim 2048 --dtype bf16]
 """
@@ -14,20 +24,27 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
+from datetime import timedelta
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 
-import torch  # noqa: E402
+import torch  # noqa: E402  (importing torch does not initialise the GPU)
 import torch.distributed as dist  # noqa: E402
 
+METRIC = "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # BASELINE.json "published": {} — the reference publishes no numbers
+CHILD_ENV = "NTXENT_BENCH_RANK_CHILD"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -35,7 +52,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=4096, help="pairs (per view) per GPU")
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
-    ap.add_argument("--compute", default="auto", choices=["auto", "fp16", "bf16", "fp32"])
+    ap.add_argument("--compute", default="auto", choices=["auto", "fp16", "bf16", "fp32", "fp8"])
     ap.add_argument("--temperature", type=float, default=0.07)
     ap.add_argument("--recompute", action="store_true", help="recompute logits in backward")
     ap.add_argument("--no-overlap", action="store_true")
@@ -45,71 +62,222 @@ def parse():
                          "its whole row block against the gathered rows; ring = O(local) memory")
     ap.add_argument("--data", default="views", choices=["views", "iid"],
                     help="views: two noisy views of a shared random-normal basis (positives correlated, "
-                         "as from a SimCLR encoder; what build/bin/ntxent_bench uses); iid: independent "
-                         "random-normal rows")
+                         "as from a SimCLR encoder); iid: independent random-normal rows")
     ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
                     help="torch: unfused PyTorch NT-Xent (hipBLASLt GEMM + eager softmax / cross-entropy, "
                          "the reference's cuBLAS-GEMM + row-kernel design) as an on-device baseline; 1 GPU")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl = RCCL over xGMI (production); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (GPU default); gloo = CPU transport (--device cpu, or the "
+                         "--share-gpu rehearsal of N ranks on one GPU)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: run the same launcher / timing / JSON path on CPU tensors (plumbing tests)")
     ap.add_argument("--share-gpu", action="store_true", help="all ranks on cuda:0 (rehearsal with gloo)")
     ap.add_argument("--graph", action="store_true",
                     help="capture one full fwd+bwd step in a hipGraph (torch.cuda.CUDAGraph) and replay it "
                          "every step (1 GPU)")
+    ap.add_argument("--secondary-fp32", default="auto", choices=["auto", "on", "off"],
+                    help="also time the exact-fp32 MFMA path (fp32 inputs, fp32 compute) at the same shape "
+                         "(auto: on for 1 GPU)")
+    ap.add_argument("--timeout", type=float, default=1500.0,
+                    help="launcher: seconds before the whole job is killed; ranks: process-group timeout")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    a = parse()
+# ------------------------------------------------------------------------------------------
+# launcher (no GPU access in this process)
+# ------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(a, argv) -> int:
+    """Start a.gpus rank processes of this script and relay rank 0's JSON line."""
+    n = a.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **{CHILD_ENV: "1"})
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+        cmd = [sys.executable, "-u", str(Path(__file__).resolve()), *argv]
+        # rank 0's stdout carries the JSON line; every rank's stderr passes through
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      stderr=None, start_new_session=True, text=True))
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
+    deadline = time.time() + a.timeout
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with code {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() > deadline:
+            failed = f"timeout after {a.timeout:.0f} s"
+            break
+        time.sleep(0.2)
+    if failed:
+        kill_all()  # before reading: a rank blocked in a collective would never close its pipe
+    out = procs[0].stdout.read() if procs[0].stdout else ""
+    if failed:
+        sys.stderr.write(f"bench launcher: {failed}; rank 0 stdout:\n{out}\n")
+        return 1
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if len(lines) != 1:
+        sys.stderr.write(f"bench launcher: expected one JSON line from rank 0, got {len(lines)}:\n{out}\n")
+        return 1
+    rec = json.loads(lines[0])
+    if rec.get("n_gpus") != n or rec.get("world_size_seen") != n:
+        sys.stderr.write(f"bench launcher: rank 0 reports n_gpus={rec.get('n_gpus')} "
+                         f"world_size_seen={rec.get('world_size_seen')}, expected {n}\n")
+        return 1
+    print(lines[0], flush=True)
+    if a.json_out:
+        Path(a.json_out).write_text(lines[0] + "\n")
+    return 0
+
+
+# ------------------------------------------------------------------------------------------
+# one rank
+# ------------------------------------------------------------------------------------------
+def _stats(ms):
+    m = sum(ms) / len(ms)
+    sd = math.sqrt(sum((x - m) ** 2 for x in ms) / len(ms)) if len(ms) > 1 else 0.0
+    return {"mean": round(m, 4), "std": round(sd, 4), "min": round(min(ms), 4), "max": round(max(ms), 4)}
+
+
+def run_rank(a) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world and world != 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    dev_index = 0 if a.share_gpu else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
+    if a.gpus != world:
+        raise SystemExit(f"bench: --gpus {a.gpus} but this process belongs to a job of WORLD_SIZE={world} "
+                         f"(run `python bench.py --gpus {a.gpus}` to launch the ranks, or torchrun with "
+                         f"--nproc-per-node {a.gpus})")
+    on_gpu = a.device == "cuda"
+    backend = a.backend or ("nccl" if on_gpu else "gloo")
+    if not on_gpu and backend != "gloo":
+        raise SystemExit("--device cpu needs the gloo backend")
+    if on_gpu:
+        dev_index = 0 if a.share_gpu else local_rank
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
+    else:
+        dev = torch.device("cpu")
+        torch.set_num_threads(max(1, min(4, (os.cpu_count() or 1) // max(1, world))))
+    world_seen = 1
     if world > 1:
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+        kw = {"timeout": timedelta(seconds=a.timeout)}
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, **kw)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **kw)
+        world_seen = dist.get_world_size()
+        if world_seen != world:
+            raise SystemExit(f"process group has {world_seen} ranks, expected {world}")
+    if os.environ.get("NTXENT_BENCH_FAIL_RANK") == str(rank):  # fault injection (launcher tests)
+        raise SystemExit(3)
 
     import ntxent_amd
-    from ntxent_amd.parallel import dist_ntxent_loss
+    from ntxent_amd.ops.reference import flops_fwd_bwd
+    from ntxent_amd.ops.reference import ntxent_loss as torch_ntxent
+    from ntxent_amd.parallel import commstats, dist_ntxent_loss
 
-    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    R = 2 * a.batch
-    if a.data == "views":  # positive pairs share a random-normal basis: view = basis + 0.5 noise
-        base = torch.randn(a.batch, a.dim, device=dev, generator=g)
-        v1 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
-        v2 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
-        h = torch.cat([v1, v2], 0).to(dt).requires_grad_(True)
-        del base, v1, v2
-    else:
-        h = torch.randn(R, a.dim, device=dev, dtype=dt, generator=g).requires_grad_(True)
     if a.impl == "torch" and world > 1:
         raise SystemExit("--impl torch is a single-GPU baseline")
+    R = 2 * a.batch
 
-    one = torch.ones((), device=dev)  # d(loss)/d(loss), allocated once outside the timed loop
+    def make_input(dtype):
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234 + rank)
+        if a.data == "views":  # positive pairs share a random-normal basis: view = basis + 0.5 noise
+            base = torch.randn(a.batch, a.dim, device=dev, generator=g)
+            v1 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
+            v2 = base + 0.5 * torch.randn(a.batch, a.dim, device=dev, generator=g)
+            return torch.cat([v1, v2], 0).to(dtype).requires_grad_(True)
+        return torch.randn(R, a.dim, device=dev, generator=g).to(dtype).requires_grad_(True)
 
-    def step():
-        if a.impl == "torch":
-            from ntxent_amd.ops.reference import ntxent_loss as torch_ntxent
-            loss = torch_ntxent(h, a.temperature)
-        elif world > 1:
-            loss = dist_ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute,
-                                    overlap=not a.no_overlap, negatives=a.negatives)
-        else:
-            loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=a.compute, keep_logits=not a.recompute)
-        (gh,) = torch.autograd.grad(loss, h, grad_outputs=one)
-        return loss, gh
+    def make_step(h, compute):
+        one = torch.ones((), device=dev, dtype=torch.float32 if h.dtype != torch.float64 else h.dtype)
 
-    if a.graph:
+        def step():
+            if a.impl == "torch":
+                loss = torch_ntxent(h, a.temperature)
+            elif world > 1:
+                loss = dist_ntxent_loss(h, a.temperature, compute=compute, keep_logits=not a.recompute,
+                                        overlap=not a.no_overlap, negatives=a.negatives)
+            else:
+                loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=compute, keep_logits=not a.recompute)
+            (gh,) = torch.autograd.grad(loss, h, grad_outputs=one.to(loss.dtype))
+            return loss, gh
+        return step
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    def barrier():
         if world > 1:
+            dist.barrier()
+
+    def timed(step, steps, warmup, per_step_events=True, comm=False):
+        """warmup untimed steps, then exactly `steps` steps bracketed by barrier + synchronize
+        on both sides; returns (total s, per-step ms list or None, comm ms per step or None)."""
+        for _ in range(warmup):
+            loss, gh = step()
+        sync()
+        barrier()
+        sync()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)] if (on_gpu and per_step_events) else None
+        if comm:
+            commstats.enable(True)
+        t0 = time.perf_counter()
+        if evs:
+            evs[0].record()
+        for i in range(steps):
+            loss, gh = step()
+            if evs:
+                evs[i + 1].record()
+        sync()
+        barrier()
+        sync()
+        dt = time.perf_counter() - t0
+        per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else None
+        comm_ms = None
+        if comm:
+            c = commstats.collect()
+            commstats.enable(False)
+            comm_ms = {k: v / steps for k, v in c.items()}
+        return dt, per, comm_ms, loss, gh
+
+    dt_in = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    h = make_input(dt_in)
+    step = make_step(h, a.compute)
+    if a.graph:
+        if world > 1 or not on_gpu:
             raise SystemExit("--graph is a single-GPU mode")
         side = torch.cuda.Stream()  # warm-up (plans, scratch, tile lists) outside the capture
         side.wait_stream(torch.cuda.current_stream())
@@ -120,46 +288,67 @@ def main():
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             g_loss, g_gh = step()
-        eager_step = step
 
         def step():  # noqa: F811 - every replay runs the complete forward + backward
             graph.replay()
             return g_loss, g_gh
 
-    for _ in range(a.warmup):
-        loss, gh = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss, gh = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt_s = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt_s], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt_s = float(t.item())
-    ms = dt_s / a.steps * 1e3
-    samples = world * a.batch
-    value = samples / (ms / 1e3)
+    if on_gpu:
+        torch.cuda.reset_peak_memory_stats(dev)
+    dt_s, per_ms, comm_ms, loss, gh = timed(step, a.steps, a.warmup, comm=world > 1)
+    peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20 if on_gpu else None
     lossv = float(loss.item())
-    if not (lossv == lossv) or not torch.isfinite(gh).all():
-        raise SystemExit("non-finite loss or gradient")
-    from ntxent_amd.ops.reference import flops_fwd_bwd
+    finite = bool(lossv == lossv and torch.isfinite(gh).all().item())
+
+    def rank_max(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def rank_all(x: float):
+        if world == 1:
+            return [x]
+        t = torch.zeros(world, dtype=torch.float64, device=dev)
+        t[rank] = x
+        dist.all_reduce(t)  # SUM of one-hot slots = gather
+        return [float(v) for v in t.cpu()]
+
+    dt_s = rank_max(dt_s)
+    ok = rank_max(0.0 if finite else 1.0) == 0.0
+    ms = dt_s / a.steps * 1e3
+    value = world * a.batch / (ms / 1e3)
+    comm_total = sum(comm_ms.values()) if comm_ms else 0.0
+    comm_all = rank_all(comm_total) if world > 1 else None
+    peak_all = rank_all(peak_mb) if peak_mb is not None and world > 1 else None
+
+    secondary = None
+    want_fp32 = a.secondary_fp32 == "on" or (a.secondary_fp32 == "auto" and world == 1 and on_gpu
+                                             and a.impl == "fused" and a.dtype != "fp32" and not a.graph)
+    if want_fp32:
+        del h, step, gh
+        h32 = make_input(torch.float32)
+        s32 = make_step(h32, "fp32")
+        n32 = max(2, min(5, a.steps // 4))
+        dt32, per32, _, _, _ = timed(s32, n32, 1)
+        ms32 = rank_max(dt32) / n32 * 1e3
+        secondary = {"dtype": "fp32", "mfma_dtype": "fp32 (exact, v_mfma_f32_16x16x4_f32)", "steps": n32,
+                     "ms_per_step": round(ms32, 4), "value": round(world * a.batch / (ms32 / 1e3), 1)}
+        del h32, s32
 
     tflops = flops_fwd_bwd(R, world * R, a.dim,
                            symmetric_global=world > 1 and a.negatives == "symmetric") / (ms / 1e3) / 1e12
     if rank == 0:
+        if not ok:
+            raise SystemExit("non-finite loss or gradient")
+        mfma = a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")
         out = {
-            "metric": "NT-Xent fwd+bwd samples/sec, B=4096 d=2048, at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
+            "world_size_seen": world_seen,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms, 4),
@@ -170,7 +359,8 @@ def main():
             "data": ("synthetic random-normal two-view embeddings (view = shared N(0,1) basis + 0.5 N(0,1))"
                      if a.data == "views" else "synthetic iid random-normal embeddings"),
             "config": {
-                "model": ("NT-Xent loss (SimCLR), fused MFMA fwd+bwd" if a.impl == "fused"
+                "model": ("NT-Xent loss (SimCLR), torch CPU path (plumbing only)" if not on_gpu
+                          else "NT-Xent loss (SimCLR), fused MFMA fwd+bwd" if a.impl == "fused"
                           else "NT-Xent loss (SimCLR), unfused PyTorch baseline (hipBLASLt + eager)"),
                 "global_batch": world * a.batch,
                 "seq_len": None,
@@ -178,24 +368,44 @@ def main():
                 "dim": a.dim,
                 "temperature": a.temperature,
                 "compute": a.compute,
-                "mfma_dtype": (a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")),
+                "mfma_dtype": mfma,
                 "keep_logits": not a.recompute,
                 "parallelism": f"dp{world}",
                 "negatives": a.negatives if world > 1 else None,
+                "backend": backend if world > 1 else None,
                 "hip_graph": bool(a.graph),
+                "device": a.device,
             },
+            "step_ms": _stats(per_ms) if per_ms else None,
+            "peak_hbm_mb": round(peak_mb, 1) if peak_mb is not None else None,
+            "peak_hbm_mb_per_rank": [round(x, 1) for x in peak_all] if peak_all else None,
+            "comm_wait_ms_per_step": {k: round(v, 4) for k, v in comm_ms.items()} if comm_ms else None,
+            "comm_wait_ms_per_step_per_rank": [round(x, 4) for x in comm_all] if comm_all else None,
+            "comm_wait_fraction_max": (round(max(comm_all) / ms, 4) if comm_all else None),
             "loss": lossv,
             "note": ("global-batch negatives: each rank's rows meet all N*B negatives, so per-GPU similarity "
                      "work grows linearly with N and the ideal whole-job samples/s is flat in N"
                      if world > 1 else None),
             "tflops_per_gpu_useful": round(tflops, 1),
+            "secondary": secondary,
         }
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             Path(a.json_out).write_text(line + "\n")
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        raise SystemExit(launch(a, argv))  # launcher: no GPU access in this process
+    run_rank(a)
 
 
 if __name__ == "__main__":

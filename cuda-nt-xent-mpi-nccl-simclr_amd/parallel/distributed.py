@@ -25,6 +25,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
+from .commstats import span
 
 
 def _world(group) -> tuple[int, int]:
@@ -103,15 +104,17 @@ class DistNTXentFunction(torch.autograd.Function):
         # own-rank (upper-triangular) tiles need only this rank's slot: they overlap the gather
         C.fwd_stats_range(fwd, fwd_all, plan, part, sc, 0, plan.n_own_tiles)
         if work_z is not None:
-            work_z.wait()
+            with span("fwd_rows"):
+                work_z.wait()
         C.fwd_stats_range(fwd, fwd_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles)
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
         if W > 1:
             mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
-            _all_gather_into(lse2_all, mine, group)
-            dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
+            with span("lse_loss"):
+                _all_gather_into(lse2_all, mine, group)
+                dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
         ctx.plan = plan
         ctx.group = group
         ctx.backward_mode = backward_mode
@@ -125,7 +128,8 @@ class DistNTXentFunction(torch.autograd.Function):
         C = _ext.load()
         h, zq, zq_all, zqt_all, inv, lse2_all, cpos = ctx.saved_tensors
         if ctx.work_t is not None:
-            ctx.work_t.wait()
+            with span("bwd_rows"):
+                ctx.work_t.wait()
             ctx.work_t = None
         sc, ctx.sc = ctx.sc, None
         if ctx.backward_mode == "reduce_scatter":
@@ -170,7 +174,8 @@ def _reduce_scatter_backward(plan, h, zq, zqt_all, inv, lse2_all, grad_out, grou
     g_cols = (D.t() @ z) * scale                         # d(own terms)/d(every row), column part
     if W > 1:
         mine = torch.empty((R, d), dtype=torch.float32, device=h.device)
-        _reduce_scatter_sum(mine, g_cols.contiguous(), group)
+        with span("bwd_reduce_scatter"):
+            _reduce_scatter_sum(mine, g_cols.contiguous(), group)
     else:
         mine = g_cols
     dz = g_rows + mine

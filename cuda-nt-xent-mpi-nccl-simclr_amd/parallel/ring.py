@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from ..ops import _ext
 from ..ops.ntxent import resolve_compute
+from .commstats import span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 _TILE_CACHE: Dict[tuple, Dict[int, torch.Tensor]] = {}
@@ -84,8 +85,9 @@ def _ring(zq: torch.Tensor, group, fn):
             nxt = bufs[s % 2]
             works = _exchange(cur, nxt, group)
         fn(q, cur)
-        for w in works:
-            w.wait()
+        with span("ring_rows"):
+            for w in works:
+                w.wait()
         if nxt is not None:
             cur = nxt
 
@@ -110,8 +112,9 @@ class RingNTXentFunction(torch.autograd.Function):
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
         if W > 1:
             mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
-            _all_gather_into(lse2_all, mine, group)
-            dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
+            with span("lse_loss"):
+                _all_gather_into(lse2_all, mine, group)
+                dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
         ctx.plan, ctx.group = plan, group
         ctx.save_for_backward(h, zq, inv, lse2_all, cpos)
         return loss

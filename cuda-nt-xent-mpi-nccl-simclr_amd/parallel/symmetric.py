@@ -40,6 +40,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
+from .commstats import span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 Job = Tuple[int, int, int, int, int]  # (q, m0, m1, k0, k1): my row tiles [m0,m1) x q's row tiles [k0,k1)
@@ -200,25 +201,29 @@ class SymNTXentFunction(torch.autograd.Function):
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
         C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)  # overlaps chunk 0
         for ws, (first, count) in zip(works, sym_chunk_segments(plan, jobs, nch)):
-            for w in ws:
-                w.wait()
+            with span("fwd_rows"):
+                for w in ws:
+                    w.wait()
             C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
-        for w in works_f16:
-            w.wait()
+        with span("fwd_rows"):
+            for w in works_f16:
+                w.wait()
         # column partials of the cross tiles -> their rows' owners (part slots [r*rt + m0, r*rt + m1))
         sends = [(part_x[q * rt + m0:q * rt + m1, k0 * 256:k1 * 256].contiguous(), q) for (q, m0, m1, k0, k1) in jobs]
         recvs = [(torch.empty((m1 - m0, (k1 - k0) * 256, 2), dtype=torch.float32, device=dev), p)
                  for (p, m0, m1, k0, k1) in inc]
-        for w in _p2p(sends, recvs, group):
-            w.wait()
+        with span("fwd_col_partials"):
+            for w in _p2p(sends, recvs, group):
+                w.wait()
         for (buf, _), (p, m0, m1, k0, k1) in zip(recvs, inc):
             part[p * rt + m0:p * rt + m1, k0 * 256:k1 * 256].copy_(buf)
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=dev)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=dev)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
         mine = lse2_all[r * Rpad:(r + 1) * Rpad].clone()
-        _all_gather_into(lse2_all, mine, group)
-        dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
+        with span("lse_loss"):
+            _all_gather_into(lse2_all, mine, group)
+            dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=group)
         ctx.plan, ctx.group = plan, group
         ctx.sc = sc
         ctx.save_for_backward(h, inv, zq_all, zqt_all, lse2_all, cpos, tiles)
@@ -344,8 +349,9 @@ def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc
     own, recv, views = sym_grad_slabs(plan, W, r, h.device)
     works = _p2p([(t, q) for q, t in contrib.items()], [(v, p) for p, v in views.items()], group)
     sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
-    for w in works:
-        w.wait()
+    with span("bwd_partner_grads"):
+        for w in works:
+            w.wait()
     del contrib, cbuf, mbuf
     return sym_norm_bwd(C, plan, own, recv, h, inv, grad_out)
 

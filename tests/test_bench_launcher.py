@@ -1,0 +1,64 @@
+"""bench.py as its own multi-rank launcher (VERDICT r1 "Next round" item 1).
+
+`python bench.py --gpus N` with no WORLD_SIZE must start N rank processes itself, relay ONE
+JSON line whose n_gpus / world_size_seen are N, fail loudly when a rank fails, and never run
+fewer ranks than asked. Driven here with --device cpu (gloo, CPU tensors): the launcher,
+rendezvous, timing brackets, rank-max reduction and JSON assembly are the same code the GPU
+run uses.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+BENCH = str(ROOT / "bench.py")
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True, timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("n,negatives", [(2, "symmetric"), (3, "allgather")])
+def test_launcher_spawns_ranks_and_relays_one_json_line(n, negatives):
+    r = _run(["--device", "cpu", "--gpus", str(n), "--batch", "16", "--dim", "8", "--steps", "3", "--warmup", "1",
+              "--dtype", "fp32", "--negatives", negatives])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["world_size_seen"] == n
+    assert d["steps"] == 3 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == n * 16 and d["config"]["parallelism"] == f"dp{n}"
+    assert d["value"] == pytest.approx(n * 16 / (d["ms_per_step"] / 1e3), rel=1e-3)
+    assert len(d["comm_wait_ms_per_step_per_rank"]) == n
+    assert d["loss"] == d["loss"]  # finite
+
+
+def test_rank_failure_fails_the_job():
+    r = _run(["--device", "cpu", "--gpus", "2", "--batch", "8", "--dim", "8", "--steps", "2", "--warmup", "1",
+              "--dtype", "fp32", "--timeout", "120"], {"NTXENT_BENCH_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert "rank 1 exited with code 3" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _run(["--device", "cpu", "--gpus", "8", "--batch", "8", "--dim", "8"], {"WORLD_SIZE": "1"})
+    assert r.returncode != 0 and "--gpus 8" in r.stderr
+
+
+def test_single_rank_cpu_json_contract():
+    r = _run(["--device", "cpu", "--batch", "16", "--dim", "8", "--steps", "2", "--warmup", "1", "--dtype", "fp32"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
