@@ -141,7 +141,8 @@ void* upload(std::vector<float>& host, DType in) {
 
 class Bench {
  public:
-  Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed)
+  Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed,
+        bool small_path = true, int small_splits = 0)
       : in_(in) {
     EngineConfig c;
     c.rows = 2 * batch;
@@ -150,6 +151,8 @@ class Bench {
     c.input = in;
     c.compute = comp;
     c.keep_cos = keep_cos;
+    c.small_path = small_path;
+    c.small_splits = small_splits;
     host_ = synthetic_views(c.rows, dim, seed);
     h_ = upload(host_, in);
     NTXENT_HIP_CHECK(hipMalloc(&dh_, host_.size() * dtype_size(in)));
@@ -257,7 +260,8 @@ struct Options {
   int batch = 0, dim = 0, iters = 100, warmup = 1, gpus = 1;
   std::string dtype = "bf16", compute = "auto", json;
   float T = 0.07f;
-  bool check = false, graph = false, recompute = false;
+  bool check = false, graph = false, recompute = false, small = true;
+  int small_splits = 0;
 };
 
 // Minimal reusable thread barrier (C++17).
@@ -338,10 +342,13 @@ int main(int argc, char** argv) {
     else if (a == "--check") o.check = true;
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
+    else if (a == "--no-small") o.small = false;
+    else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
-                  "                    [--recompute] [--gpus N] [--json out.json]\n");
+                  "                    [--recompute] [--no-small] [--gpus N] [--json out.json]\n"
+                  "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n");
       return 0;
     }
   }
@@ -365,28 +372,29 @@ int main(int argc, char** argv) {
     for (int b : {32, 64, 128, 256, 512, 1024})
       for (int d : {64, 128, 256}) shapes.push_back({b, d});
   }
-  std::printf("%6s %6s %5s | %-38s | %-38s | %-38s | %-10s | %12s %9s\n", "B", "D", "dtype",
+  std::printf("%6s %6s %5s %5s | %-38s | %-38s | %-38s | %-10s | %12s %9s\n", "B", "D", "dtype", "path",
               "fwd ms: mean / std / min / max", "bwd ms: mean / std / min / max",
               "fwd+bwd ms: mean / std / min / max", "graph ms", "samples/s", "TFLOP/s");
   FILE* jf = o.json.empty() ? nullptr : std::fopen(o.json.c_str(), "w");
   if (jf) std::fprintf(jf, "{\"device\": \"%s\", \"results\": {", di.arch.c_str());
   bool first = true;
   for (auto [b, d] : shapes) {
-    Bench bench(b, d, in, comp, o.T, !o.recompute, nullptr, 1234);
+    Bench bench(b, d, in, comp, o.T, !o.recompute, nullptr, 1234, o.small, o.small_splits);
+    const char* path = bench.engine().small() ? "small" : "large";
     const Result f = stats(bench.time(0, o.warmup, o.iters));
     const Result bw = stats(bench.time(1, o.warmup, o.iters));
     const Result fb = stats(bench.time(2, o.warmup, o.iters));
     const Result gr = o.graph ? stats(bench.time(3, o.warmup, o.iters)) : Result{};
     const double best = o.graph ? std::min(gr.mean, fb.mean) : fb.mean;
     const double tf = step_flops(bench.geom()) / (best * 1e-3) / 1e12;
-    std::printf("%6d %6d %5s | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %10.4f | %12.1f %9.1f\n",
-                b, d, o.dtype.c_str(), f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn, bw.mx, fb.mean,
+    std::printf("%6d %6d %5s %5s | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %8.4f %8.4f %8.4f %8.4f   | %10.4f | %12.1f %9.1f\n",
+                b, d, o.dtype.c_str(), path, f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn, bw.mx, fb.mean,
                 fb.stdev, fb.mn, fb.mx, gr.mean, b / (best * 1e-3), tf);
     if (jf) {
-      std::fprintf(jf, "%s\n  \"B=%d,d=%d,dtype=%s,world=1\": {\"fwd_ms\": [%.5f, %.5f, %.5f, %.5f], "
+      std::fprintf(jf, "%s\n  \"B=%d,d=%d,dtype=%s,world=1\": {\"path\": \"%s\", \"fwd_ms\": [%.5f, %.5f, %.5f, %.5f], "
                    "\"bwd_ms\": [%.5f, %.5f, %.5f, %.5f], \"fwd_bwd_ms\": [%.5f, %.5f, %.5f, %.5f], "
                    "\"graph_ms\": %.5f, \"samples_per_s\": %.1f, \"tflops\": %.2f, \"device_bytes\": %zu}",
-                   first ? "" : ",", b, d, o.dtype.c_str(), f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn,
+                   first ? "" : ",", b, d, o.dtype.c_str(), path, f.mean, f.stdev, f.mn, f.mx, bw.mean, bw.stdev, bw.mn,
                    bw.mx, fb.mean, fb.stdev, fb.mn, fb.mx, gr.mean, b / (best * 1e-3), tf,
                    bench.engine().device_bytes());
       first = false;

@@ -41,6 +41,8 @@ struct EngineConfig {
 #endif
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
   bool check_finite = false;  // loss() throws on a non-finite loss
+  bool small_path = true;     // single-rank small problems: the one-launch fwd / bwd kernels
+  int small_splits = 0;       // small path: backward column splits (0: small_bwd_splits)
   int device = -1;            // -1: current device
 };
 
@@ -77,6 +79,7 @@ class Engine {
   int fwd_tiles() const { return n_fwd_; }
   int own_tiles() const { return n_own_; }
   int dz_tiles() const { return n_dz_; }
+  bool small() const { return small_; }
   Comm* comm() const { return comm_; }
 
  private:
@@ -88,6 +91,8 @@ class Engine {
   int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
+  bool small_ = false;        // small-problem path (small_kernels.hip)
+  void* small_scratch_ = nullptr;
   DType bwd_ = DType::F16;
   void* arena_ = nullptr;
   size_t arena_bytes_ = 0;

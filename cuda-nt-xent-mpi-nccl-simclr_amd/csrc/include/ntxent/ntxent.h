@@ -228,6 +228,27 @@ void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,
                      const float* inv, const float* grad_out, void* dh, const Geometry& g,
                      hipStream_t stream, const void* xslabs = nullptr, int nx = 0);
 
+// ---- small-problem path (kernels/small_kernels.hip) -------------------------------------
+// Single-rank problems with R <= kSmallMaxRows and dim_k <= kSmallMaxDk in fp16/bf16: after
+// launch_prep, ONE forward launch (64 x 64 MFMA tiles, in-kernel LSE merge and deterministic
+// loss sum) and ONE backward launch (S recomputed, C formed in registers and fed straight to
+// the dZ MFMA, normalisation backward fused). `scratch` (small_scratch_bytes) must be ZERO when
+// first used (its arrival counters return to zero after every launch); launches sharing it must
+// be stream-ordered. lse2 / arow ([small_rows_pad(g)] floats) carry the row statistics from the
+// forward to the backward: LSE in log2 units and a_i = 1 - P_i,p(i).
+constexpr int kSmallMaxRows = 2048;
+constexpr int kSmallMaxDk = 256;
+bool small_path_eligible(const Geometry& g, DType comp);
+int small_bwd_splits(const Geometry& g);  // default column splits of the backward grid
+int small_rows_pad(const Geometry& g);    // roundup(R, 64)
+size_t small_scratch_bytes(const Geometry& g, int splits);
+void launch_small_fwd(DType comp, const void* zq, const float* ypos, float* lse2, float* arow, float* loss,
+                      void* scratch, const Geometry& g, hipStream_t stream);
+// splits <= 0: small_bwd_splits(g). grad_out: device fp32 scalar.
+void launch_small_bwd(DType in, DType comp, const void* zq, const void* h, const float* inv, const float* lse2,
+                      const float* arow, const float* grad_out, void* dh, void* scratch, const Geometry& g,
+                      hipStream_t stream, int splits = 0);
+
 // ---- device utilities (reference utils::get_optimal_block_size / check_tensor_core_support
 //      at include/ntxent_kernel.cuh:80-110) ------------------------------------------------
 struct DeviceInfo {

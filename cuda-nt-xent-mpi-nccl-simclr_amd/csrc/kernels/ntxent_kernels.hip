@@ -76,6 +76,19 @@ __device__ __forceinline__ u32x2 quant8(const float (&x)[8], float (&q)[8]) {
   return r;
 }
 
+// Zero one pad row of zq ([ldk] elements) and, for fp8 plans, of zq8 ([ldk8] bytes) with
+// 16-byte stores by `nt` cooperating threads.
+template <typename Tc, bool Q8>
+__device__ __forceinline__ void zero_pad_row(Tc* zq, unsigned char* zq8, int row, int ldk, int ldk8, int t, int nt) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  char* r = reinterpret_cast<char*>(zq + (long long)row * ldk);
+  for (int b = t * 16; b < ldk * (int)sizeof(Tc); b += nt * 16) *reinterpret_cast<u32x4*>(r + b) = z;
+  if constexpr (Q8) {
+    unsigned char* r8 = zq8 + (long long)row * ldk8;
+    for (int b = t * 16; b < ldk8; b += nt * 16) *reinterpret_cast<u32x4*>(r8 + b) = z;
+  }
+}
+
 // Q8: also write the fp8 copy zq8 (row stride ldk8 bytes, zero padded to dk8) used by the fp8
 // forward GEMM; the positive logit then comes from the dequantised fp8 rows, consistent with
 // the GEMM's logits.
@@ -86,6 +99,10 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
                                                    unsigned char* __restrict__ zq8, int dk8, int ldk8) {
   __shared__ float red[16];
   const int n = R >> 1, i = blockIdx.x, pi = i + n;
+  if (i >= n) {  // pad row R + (i - n) of zq (and zq8): zeros (replaces a memset launch)
+    zero_pad_row<Tc, Q8>(zq, zq8, R + (i - n), ldk, ldk8, threadIdx.x, 256);
+    return;
+  }
   const Tin* hi = h + (long long)i * d;
   const Tin* hp = h + (long long)pi * d;
   Tc* zi = zq + (long long)i * ldk;
@@ -163,9 +180,16 @@ template <typename Tin, typename Tc, bool Q8, int NCH>
 __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
                                                         float* __restrict__ inv, float* __restrict__ ypos,
                                                         int R, int d, int dk, int ldk, float y_scale,
-                                                        unsigned char* __restrict__ zq8, int dk8, int ldk8) {
+                                                        unsigned char* __restrict__ zq8, int dk8, int ldk8,
+                                                        int pad_end) {
   const int lane = threadIdx.x & 63;
   const int n = R >> 1;
+  const int npb = (n + 3) >> 2;  // pair blocks; the blocks after them zero the pad rows
+  if ((int)blockIdx.x >= npb) {
+    const int row = R + ((int)blockIdx.x - npb) * 4 + (threadIdx.x >> 6);
+    if (row < pad_end) zero_pad_row<Tc, Q8>(zq, zq8, row, ldk, ldk8, lane, 64);
+    return;
+  }
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;  // whole wave
   const int pi = i + n;
@@ -780,14 +804,9 @@ std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit) {
 void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
                  const Geometry& g, hipStream_t stream, void* zq8) {
   NTXENT_CHECK(comp != DType::FP8, "prep: pass the fp16 plan dtype and a zq8 buffer for fp8");
-  const size_t cs = dtype_size(comp);
-  if (g.rows_pad > g.rows) {
-    NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq) + (size_t)g.rows * g.ld_k * cs, 0,
-                                    (size_t)(g.rows_pad - g.rows) * g.ld_k * cs, stream));
-    if (zq8)
-      NTXENT_HIP_CHECK(hipMemsetAsync(static_cast<char*>(zq8) + (size_t)g.rows * g.ld_k8, 0,
-                                      (size_t)(g.rows_pad - g.rows) * g.ld_k8, stream));
-  }
+  // pad rows [R, Rpad) are zeroed by extra blocks of the prep kernel itself (no memset launch);
+  // zq rows are 16-byte multiples (ld_k is a multiple of 64 elements, ld_k8 of 128 bytes)
+  const int pad = g.rows_pad - g.rows;
   const float ys = g.inv_temp * dev::kLog2e;
   // wave-per-pair kernel when the rows fit in registers (d <= 2048), else one block per pair
   const int nch = (g.dim % 8 == 0) ? (g.dim + 511) / 512 : 0;
@@ -796,13 +815,13 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
     dispatch_comp(comp, [&](auto tc) {
       using Tc = decltype(tc);
       if (nch >= 1 && nch <= 4) {
-        const dim3 grid((g.rows / 2 + 3) / 4);
+        const dim3 grid((g.rows / 2 + 3) / 4 + (pad + 3) / 4);
         auto go = [&](auto nc, auto q8) {
           constexpr int NC = decltype(nc)::value;
           constexpr bool Q = decltype(q8)::value;
           hipLaunchKernelGGL((dev::prep_wave_kernel<Tin, Tc, Q, NC>), grid, dim3(256), 0, stream,
                              static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim, g.dim_k,
-                             g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8);
+                             g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8, g.rows_pad);
         };
         auto by_q = [&](auto nc) {
           if (zq8) go(nc, std::true_type{});
@@ -814,11 +833,11 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
         return;
       }
       if (zq8)
-        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, true>), dim3(g.rows / 2), dim3(256), 0, stream,
+        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, true>), dim3(g.rows / 2 + pad), dim3(256), 0, stream,
                            static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
                            g.dim_k, g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8);
       else
-        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, false>), dim3(g.rows / 2), dim3(256), 0, stream,
+        hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, false>), dim3(g.rows / 2 + pad), dim3(256), 0, stream,
                            static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
                            g.dim_k, g.ld_k, ys, nullptr, 0, 0);
     });

@@ -7,6 +7,7 @@
 // the own-rank tiles.
 #include "ntxent/engine.h"
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <vector>
@@ -36,6 +37,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   if (f8_) cfg_.keep_cos = true;  // fp8: the fp16 backward uses the forward's own cosines
   bwd_ = backward_dtype(cfg.compute);
   cs_ = dtype_size(bwd_);
+  small_ = cfg.small_path && world_ == 1 && small_path_eligible(g_, cfg.compute);
 
   const auto ft = build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_, 1);
@@ -65,6 +67,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
       {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
       {&ws_.ptr, ws_.bytes},
+      {&small_scratch_, small_ ? small_scratch_bytes(g_, std::max(small_bwd_splits(g_), cfg.small_splits)) : 0},
   };
   size_t total = 0;
   for (const auto& s : slots) total += align_up(s.bytes);
@@ -115,6 +118,13 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_TRACE("ntxent.prep");
     fault_point("prep");
     launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
+    if (small_) {  // one launch: tiles + LSE merge + loss (lse2 -> lse2_all_, a_i -> cpos_)
+      NTXENT_TRACE("ntxent.small_fwd");
+      fault_point("fwd");
+      launch_small_fwd(cfg_.compute, zq_local, ypos_, lse2_all_, cpos_, loss_, small_scratch_, g_, s);
+      if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
+      return;
+    }
     launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
@@ -156,6 +166,13 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   NTXENT_CHECK(h_ != nullptr, "backward() before forward()");
   const size_t Rp = g_.rows_pad;
   const char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
+  if (small_) {
+    NTXENT_TRACE("ntxent.small_bwd");
+    fault_point("dz");
+    launch_small_bwd(cfg_.input, cfg_.compute, zq_local, h_, inv_, lse2_all_, cpos_, grad_out ? grad_out : one_, dh,
+                     small_scratch_, g_, s, std::min(cfg_.small_splits, small_rows_pad(g_) / 64));
+    return;
+  }
   {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");

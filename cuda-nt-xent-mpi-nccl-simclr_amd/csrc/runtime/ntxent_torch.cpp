@@ -64,6 +64,7 @@ struct Plan {
   int n_dz = 0;
   int ksplit = 1;
   int num_cus = 256;
+  bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
@@ -112,6 +113,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   auto dt = build_dz_tiles(p->g, p->ksplit);
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
+  p->small = small_path_eligible(p->g, comp);
   cache.emplace(key, p);
   return p;
 }
@@ -556,6 +558,23 @@ at::Tensor norm_bwd_slabs(const at::Tensor& slabs, const at::Tensor& h, const at
 }
 
 // ---- single-process fused flows ------------------------------------------------------
+// Small-problem path switch (default on): the one-launch forward / backward of
+// small_kernels.hip for plans with Plan::small; off = the large-problem pipeline for every
+// shape (A/B tests and benchmarks).
+static bool g_small_path = true;
+static int g_small_splits = 0;  // backward column splits (0: small_bwd_splits)
+void set_small_path(bool on) { g_small_path = on; }
+bool small_path_enabled() { return g_small_path; }
+void set_small_splits(int n) { g_small_splits = std::max(0, n); }
+
+static int small_splits(const Plan& P) {
+  const int nt = small_rows_pad(P.g) / 64;
+  return g_small_splits > 0 ? std::min(g_small_splits, nt) : small_bwd_splits(P.g);
+}
+static at::Tensor small_scratch(const at::Tensor& like, const Plan& P) {
+  return device_scratch(like, small_scratch_bytes(P.g, std::max(small_splits(P), small_bwd_splits(P.g))), 2);
+}
+
 // Returns {loss, zq, zqt, inv, lse2, sc, cpos}; `sc` holds the kept cosines (keep_cos) or is
 // undefined.
 std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::string& compute, bool keep_cos) {
@@ -567,6 +586,17 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
+  if (P->small && g_small_path) {
+    // {loss, zq, -, inv, lse2, -, a}: the backward recomputes S from zq (small_bwd)
+    const int rp = small_rows_pad(P->g);
+    auto lse2 = at::empty({rp}, opts(h, at::kFloat));
+    auto arow = at::empty({rp}, opts(h, at::kFloat));
+    auto loss = at::empty({}, opts(h, at::kFloat));
+    launch_small_fwd(P->comp, pr[0].data_ptr(), pr[2].data_ptr<float>(), lse2.data_ptr<float>(),
+                     arow.data_ptr<float>(), loss.data_ptr<float>(), small_scratch(h, *P).data_ptr(), P->g,
+                     cur_stream(h));
+    return {loss, pr[0], at::Tensor(), pr[1], lse2, at::Tensor(), arow};
+  }
   static const bool side_t = [] {
     const char* e = std::getenv("NTXENT_SIDE_TRANSPOSE");
     return e == nullptr || std::atoi(e) != 0;
@@ -617,12 +647,23 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
-at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const at::Tensor& zqt, const at::Tensor& inv,
+at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::optional<at::Tensor>& zqt_in,
+                          const at::Tensor& inv,
                           const at::Tensor& lse2, const c10::optional<at::Tensor>& sc_in, const at::Tensor& cpos,
                           const at::Tensor& grad_out, double T) {
   const at::DeviceGuard guard(h.device());
   const DType comp = to_dtype(zq.scalar_type());
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
+  const at::Tensor zqt = zqt_in.has_value() ? *zqt_in : at::Tensor();
+  if (!zqt.defined()) {  // small-problem forward (see fused_forward): `cpos` holds a_i
+    NTXENT_CHECK(P->small, "fused_backward: missing ZqT for a large-problem plan");
+    auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
+    auto dh = at::empty_like(h);
+    launch_small_bwd(to_dtype(h.scalar_type()), P->comp, zq.data_ptr(), h.data_ptr(), inv.data_ptr<float>(),
+                     lse2.data_ptr<float>(), cpos.data_ptr<float>(), go.data_ptr<float>(), dh.data_ptr(),
+                     small_scratch(h, *P).data_ptr(), P->g, cur_stream(h), small_splits(*P));
+    return dh;
+  }
   at::Tensor cb;
   if (sc_in.has_value() && sc_in->defined()) {
     cb = coef(*sc_in, lse2, cpos, *P);
@@ -743,6 +784,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("ksplit", &Plan::ksplit)
+      .def_readonly("small", &Plan::small)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
   m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
@@ -779,6 +821,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);
+  m.def("set_small_path", &set_small_path, py::arg("on"));
+  m.def("small_path_enabled", &small_path_enabled);
+  m.def("set_small_splits", &set_small_splits, py::arg("n"));
   // reference API names and kwargs
   m.def("forward", &forward_op, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
   m.def("forward_with_stats", &forward_with_stats, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);

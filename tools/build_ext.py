@@ -30,6 +30,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
 RUNTIME_SRCS = ["engine.cpp", "rccl_comm.cpp", "trace.cpp"]
+KERNEL_SRCS = [CSRC / "kernels" / "ntxent_kernels.hip", CSRC / "kernels" / "small_kernels.hip"]
 
 
 def _host_cxx():
@@ -96,13 +97,15 @@ def build(force: bool = False, cpp_targets: bool = True, verbose: bool = False) 
     common = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}"]
     hdrs = _headers()
 
-    k_src = CSRC / "kernels" / "ntxent_kernels.hip"
-    k_obj = BUILD / "ntxent_kernels.o"
+    k_objs = []
     t_src = CSRC / "runtime" / "ntxent_torch.cpp"
     t_obj = BUILD / "ntxent_torch.o"
     jobs = []
-    if force or _stale(k_obj, [k_src, *hdrs]):
-        jobs.append(common + ["-O3", "-c", str(k_src), "-o", str(k_obj)])
+    for k_src in KERNEL_SRCS:
+        k_obj = BUILD / (k_src.stem + ".o")
+        k_objs.append(k_obj)
+        if force or _stale(k_obj, [k_src, *hdrs]):
+            jobs.append(common + ["-O3", "-c", str(k_src), "-o", str(k_obj)])
     if force or _stale(t_obj, [t_src, *hdrs]):
         tflags = [f"-I{p}" for p in tinc] + [
             f"-I{pyinc}",
@@ -129,15 +132,15 @@ def build(force: bool = False, cpp_targets: bool = True, verbose: bool = False) 
         list(ex.map(lambda c: _run(c, verbose), jobs))
 
     so = ext_path()
-    if force or _stale(so, [k_obj, t_obj, *rt_objs]):
+    if force or _stale(so, [*k_objs, t_obj, *rt_objs]):
         # RCCL: bind to the copy torch ships (one RCCL instance per process)
-        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(k_obj), str(t_obj), *map(str, rt_objs),
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, k_objs), str(t_obj), *map(str, rt_objs),
                 "-o", str(so), f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
                 "-ltorch_python", "-lrccl", "-ldl", f"-Wl,-rpath,{tlib}"]
         _run(link, verbose)
 
     if cpp_targets:
-        build_cpp_targets([k_obj, *rt_objs], force=force, verbose=verbose)
+        build_cpp_targets([*k_objs, *rt_objs], force=force, verbose=verbose)
     return so
 
 
@@ -173,10 +176,11 @@ def build_sanitized(verbose: bool = False) -> Path:
     out_dir.mkdir(parents=True, exist_ok=True)
     inc = f"-I{CSRC / 'include'}"
     objs = []
-    k_obj = out_dir / "ntxent_kernels.o"
-    _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", inc, "-O2", *SAN, "-c",
-          str(CSRC / "kernels" / "ntxent_kernels.hip"), "-o", str(k_obj)], verbose)
-    objs.append(k_obj)
+    for k_src in KERNEL_SRCS:
+        k_obj = out_dir / (k_src.stem + ".o")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", inc, "-O2", *SAN, "-c", str(k_src), "-o",
+              str(k_obj)], verbose)
+        objs.append(k_obj)
     for name in RUNTIME_SRCS:
         obj = out_dir / (Path(name).stem + ".o")
         _run(_host_cxx() + [inc, "-O1", *SAN, "-c", str(CSRC / "runtime" / name), "-o", str(obj)], verbose)

@@ -13,6 +13,6 @@ timeout -k 10 300 python bench.py > $OUT/bench1.log 2>&1 || { echo "bench1 faile
 tail -1 $OUT/bench1.log | cut -c1-300
 timeout -k 10 300 python bench.py --gpus 2 --steps 3 --warmup 1 --backend gloo --share-gpu > $OUT/bench_launch2.log 2>&1 || { echo "launcher N=2 failed"; tail -20 $OUT/bench_launch2.log; exit 1; }
 tail -1 $OUT/bench_launch2.log | cut -c1-200
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --steps 10 --warmup 3 --secondary-fp32 off > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --secondary-fp32 off > $OUT/prof.log 2>&1 || { echo "rocprof failed"; tail -20 $OUT/prof.log; exit 1; }
 find $OUT/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} $OUT/kernel_stats.csv
 echo done
