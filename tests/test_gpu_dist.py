@@ -5,6 +5,7 @@ The 2/4/8-GPU runs happen on the driver's 8-GPU node; what they execute per rank
 column tiles, global column indices, per-rank LSE slots, rank-local symmetric backward) is
 verified here against the fp64 oracle on the gathered batch.
 """
+import contextlib
 import os
 import socket
 
@@ -58,17 +59,39 @@ def test_emulated_ranks_match_oracle(W, n, dim, compute, keep):
         assert err <= gt * scale, (r, err, scale)
 
 
+@contextlib.contextmanager
+def _large_path():
+    """Force the large-problem pipeline for single-GPU calls (shapes here would otherwise take
+    the one-launch small-problem path, which rounds differently)."""
+    from ntxent_amd.ops import _ext
+
+    mod = _ext.load(build_if_missing=False)
+    mod.set_small_path(False)
+    try:
+        yield
+    finally:
+        mod.set_small_path(True)
+
+
 def test_emulated_world1_equals_single_gpu():
     import ntxent_amd
     from ntxent_amd.parallel.emulate import emulated_dist_forward_backward
 
     h = _shards(1, 300, 96, seed=5)[0].float().cuda()
     loss, (g,) = emulated_dist_forward_backward([h], 0.07, compute="fp16")
-    x = h.clone().requires_grad_(True)
-    l2 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
-    (g2,) = torch.autograd.grad(l2, x)
+    # the emulated ranks run the large-problem pipeline: bitwise equal to it at world 1
+    with _large_path():
+        x = h.clone().requires_grad_(True)
+        l2 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
+        (g2,) = torch.autograd.grad(l2, x)
     assert loss.item() == l2.item()
     assert torch.equal(g, g2)
+    # ... and within rounding of the single-launch small-problem path this shape selects
+    x = h.clone().requires_grad_(True)
+    l3 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
+    (g3,) = torch.autograd.grad(l3, x)
+    assert abs(l3.item() - l2.item()) <= 1e-4 * max(1.0, abs(l2.item()))
+    assert (g3 - g2).abs().max().item() <= 2e-3 * g2.abs().max().item()
 
 
 def _free_port():
@@ -102,9 +125,10 @@ def test_rccl_path_world1(nccl_world1, overlap):
     x = h.clone().requires_grad_(True)
     loss = dist_ntxent_loss(x, 0.07, overlap=overlap)
     (g,) = torch.autograd.grad(loss, x)
-    y = h.clone().requires_grad_(True)
-    l2 = ntxent_amd.ntxent_loss(y, 0.07)
-    (g2,) = torch.autograd.grad(l2, y)
+    with _large_path():  # the data-parallel path runs the large-problem pipeline
+        y = h.clone().requires_grad_(True)
+        l2 = ntxent_amd.ntxent_loss(y, 0.07)
+        (g2,) = torch.autograd.grad(l2, y)
     assert loss.item() == l2.item()
     assert torch.equal(g, g2)
 
