@@ -138,7 +138,12 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus);
 struct GemmWorkspace {
   void* ptr = nullptr;
   size_t bytes = 0;
-  int num_cus = 256;
+  int num_cus = 256;    // sizes the counter region and the slabs (the device's CU count)
+  // Grid cap of the persistent schedule (0: num_cus). A GEMM launched while an RCCL transfer is
+  // in flight leaves num_cus - sched_cus CUs free for the communication kernels: the persistent
+  // blocks (128 KiB LDS, the whole register file) would otherwise hold every CU until the GEMM
+  // ends and the "overlapped" transfer would start only then.
+  int sched_cus = 0;
 };
 size_t gemm_workspace_bytes(int ntiles, int num_cus);
 

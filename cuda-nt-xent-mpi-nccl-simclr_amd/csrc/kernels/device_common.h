@@ -62,22 +62,23 @@ template <> struct Mfma<float> {
   }
 };
 
-// fp8 e4m3 (OCP, gfx950) operand type: the 128-byte K-step of a row holds 128 elements; a
-// 16-byte fragment feeds TWO v_mfma_f32_16x16x32_fp8_fp8 (its low and high 8 bytes). Lane l
-// of the fragment holds elements 16c..16c+15 of its chunk c, so each MFMA sums a fixed
-// permutation of 32 k positions — the same one for A and B, hence the exact dot product.
+// fp8 e4m3 (OCP, gfx950) operand type: the 128-byte K-step of a row holds 128 elements and runs
+// on the CDNA4 block-scaled MFMA v_mfma_scale_f32_16x16x128_f8f6f4 (twice the fp16/bf16 and the
+// legacy 16x16x32 fp8 rate). One MFMA per (row block, column block) and K-step: lane l's 32-byte
+// operand is the concatenation of its two 16-byte chunks (k-substeps s = 0, 1), i.e. chunks
+// {cq, cq + 4} of the K-step for lane group cq = l >> 4 — a fixed permutation of the 128 k
+// positions, the same for A and B, so the dot product is exact.
+// Scales: every row of Zq8 is quantised with its own power of two 2^e (e4m3(z * 2^e), amax of
+// the row mapped into [224, 448]) and carries the E8M0 byte 127 - e; the MFMA applies
+// 2^(sa - 127) * 2^(sb - 127), so the accumulator is the unscaled dot product. A lane passes
+// the scale of its A row (l & 15 of the row block) and of its B row (= output column).
 struct fp8e4m3 {
   unsigned char v;
 };
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 template <> struct Mfma<fp8e4m3> {
-  typedef u32x4 frag;
-  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
-    const long a0 = (long)a[0] | ((long)a[1] << 32), a1 = (long)a[2] | ((long)a[3] << 32);
-    const long b0 = (long)b[0] | ((long)b[1] << 32), b1 = (long)b[2] | ((long)b[3] << 32);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a0, b0, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a1, b1, c, 0, 0, 0);
-    return c;
-  }
+  typedef u32x4 frag;  // 16 bytes of one k-substep; the MFMA itself: mma_mx_sel in sim_gemm.h
 };
 
 // Element type used to store cosines / coefficients produced from a GEMM in operand type T
@@ -85,9 +86,14 @@ template <> struct Mfma<fp8e4m3> {
 template <typename T> struct StoreT { typedef T type; };
 template <> struct StoreT<fp8e4m3> { typedef _Float16 type; };
 
-// Per-tensor fp8 scale: normalised rows (|z| <= 1) are stored as e4m3(z * kFp8Scale); a power
-// of two, so scaling is exact and S = acc / kFp8Scale^2.
-constexpr float kFp8Scale = 256.0f;
+// Per-row fp8 scale exponent: the largest e with amax * 2^e <= 448 (e4m3 max), clamped to
+// [0, 126]; the row's E8M0 scale byte is 127 - e. amax = 0 (a zero / pad row) gives e = 126.
+__device__ __forceinline__ int fp8_row_exp(float amax) {
+  if (!(amax > 0.f)) return 126;
+  const float r = 448.0f / amax;
+  const int e = ((__float_as_int(r) >> 23) & 0xff) - 127;  // floor(log2 r) for normal r
+  return e < 0 ? 0 : (e > 126 ? 126 : e);
+}
 
 // ---- wave64 cross-lane reductions ----------------------------------------------------
 // DPP row_ror within a 16-lane row: 0x120 + n.
@@ -146,6 +152,19 @@ __device__ __forceinline__ float block_sum(float x, float* red) {
   __syncthreads();
   float t = 0.f;
   for (int i = 0; i < nw; ++i) t += red[i];  // fixed order: deterministic
+  return t;
+}
+
+// Block-wide max (same contract as block_sum).
+__device__ __forceinline__ float block_max(float x, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  x = xrow_max(row16_max(x));
+  __syncthreads();
+  if (lane == 0) red[w] = x;
+  __syncthreads();
+  float t = red[0];
+  for (int i = 1; i < nw; ++i) t = fmaxf(t, red[i]);
   return t;
 }
 

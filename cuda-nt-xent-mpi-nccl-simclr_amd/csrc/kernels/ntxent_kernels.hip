@@ -58,20 +58,21 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
   }
 }
 
-// fp8 e4m3 of 8 values (x * kFp8Scale), packed little-endian into 2 dwords; q receives the
-// dequantised values (what the fp8 GEMM multiplies), divided back by the scale.
-__device__ __forceinline__ u32x2 quant8(const float (&x)[8], float (&q)[8]) {
+// fp8 e4m3 of 8 values (x * sc, sc = 2^e the row's scale), packed little-endian into 2 dwords;
+// q receives the dequantised values (what the fp8 GEMM multiplies), divided back by sc.
+__device__ __forceinline__ u32x2 quant8(const float (&x)[8], float (&q)[8], float sc) {
   u32x2 r;
+  const float isc = 1.0f / sc;  // exact: sc is a power of two
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     int v = 0;
-    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * kFp8Scale, x[4 * h + 1] * kFp8Scale, v, false);
-    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 2] * kFp8Scale, x[4 * h + 3] * kFp8Scale, v, true);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h] * sc, x[4 * h + 1] * sc, v, false);
+    v = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 2] * sc, x[4 * h + 3] * sc, v, true);
     r[h] = (unsigned)v;
-    q[4 * h + 0] = __builtin_amdgcn_cvt_f32_fp8(v, 0) * (1.0f / kFp8Scale);
-    q[4 * h + 1] = __builtin_amdgcn_cvt_f32_fp8(v, 1) * (1.0f / kFp8Scale);
-    q[4 * h + 2] = __builtin_amdgcn_cvt_f32_fp8(v, 2) * (1.0f / kFp8Scale);
-    q[4 * h + 3] = __builtin_amdgcn_cvt_f32_fp8(v, 3) * (1.0f / kFp8Scale);
+    q[4 * h + 0] = __builtin_amdgcn_cvt_f32_fp8(v, 0) * isc;
+    q[4 * h + 1] = __builtin_amdgcn_cvt_f32_fp8(v, 1) * isc;
+    q[4 * h + 2] = __builtin_amdgcn_cvt_f32_fp8(v, 2) * isc;
+    q[4 * h + 3] = __builtin_amdgcn_cvt_f32_fp8(v, 3) * isc;
   }
   return r;
 }
@@ -108,25 +109,36 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
   Tc* zi = zq + (long long)i * ldk;
   Tc* zp = zq + (long long)pi * ldk;
   const bool vec = (d % 8) == 0;
-  float ssi = 0.f, ssp = 0.f;
+  float ssi = 0.f, ssp = 0.f, mxi = 0.f, mxp = 0.f;  // sums of squares, max |h| (fp8 row scales)
   if (vec) {
     for (int e = threadIdx.x * 8; e < d; e += 256 * 8) {
       float a[8], b[8];
       load8<Tin>(hi + e, a);
       load8<Tin>(hp + e, b);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { ssi += a[j] * a[j]; ssp += b[j] * b[j]; }
+      for (int j = 0; j < 8; ++j) {
+        ssi += a[j] * a[j]; ssp += b[j] * b[j];
+        mxi = fmaxf(mxi, fabsf(a[j])); mxp = fmaxf(mxp, fabsf(b[j]));
+      }
     }
   } else {
     for (int e = threadIdx.x; e < d; e += 256) {
       const float a = to_f32<Tin>(hi[e]), b = to_f32<Tin>(hp[e]);
       ssi += a * a; ssp += b * b;
+      mxi = fmaxf(mxi, fabsf(a)); mxp = fmaxf(mxp, fabsf(b));
     }
   }
   ssi = block_sum(ssi, red);
   ssp = block_sum(ssp, red + 8);
   const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
   const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  // fp8: per-row power-of-two scale from the row's amax (amax of z = amax of h * inv exactly)
+  int ei = 0, ep = 0;
+  if constexpr (Q8) {
+    ei = fp8_row_exp(block_max(mxi, red) * ivi);
+    ep = fp8_row_exp(block_max(mxp, red + 8) * ivp);
+  }
+  const float sci = __int_as_float((ei + 127) << 23), scp = __int_as_float((ep + 127) << 23);
   float dot = 0.f;
   unsigned char* zi8 = Q8 ? zq8 + (long long)i * ldk8 : nullptr;
   unsigned char* zp8 = Q8 ? zq8 + (long long)pi * ldk8 : nullptr;
@@ -140,8 +152,8 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
       store8<Tc>(zi + e, a, qa);
       store8<Tc>(zp + e, b, qb);
       if constexpr (Q8) {
-        *reinterpret_cast<u32x2*>(zi8 + e) = quant8(a, qa);
-        *reinterpret_cast<u32x2*>(zp8 + e) = quant8(b, qb);
+        *reinterpret_cast<u32x2*>(zi8 + e) = quant8(a, qa, sci);
+        *reinterpret_cast<u32x2*>(zp8 + e) = quant8(b, qb, scp);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot += qa[j] * qb[j];
@@ -153,19 +165,24 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
       const Tc b = from_f32<Tc>(bf);
       zi[e] = a; zp[e] = b;
       if constexpr (Q8) {
-        const int va = __builtin_amdgcn_cvt_pk_fp8_f32(af * kFp8Scale, 0.f, 0, false);
-        const int vb = __builtin_amdgcn_cvt_pk_fp8_f32(bf * kFp8Scale, 0.f, 0, false);
+        const int va = __builtin_amdgcn_cvt_pk_fp8_f32(af * sci, 0.f, 0, false);
+        const int vb = __builtin_amdgcn_cvt_pk_fp8_f32(bf * scp, 0.f, 0, false);
         zi8[e] = (unsigned char)(va & 0xFF);
         zp8[e] = (unsigned char)(vb & 0xFF);
-        dot += __builtin_amdgcn_cvt_f32_fp8(va, 0) * __builtin_amdgcn_cvt_f32_fp8(vb, 0) * (1.0f / (kFp8Scale * kFp8Scale));
+        dot += (__builtin_amdgcn_cvt_f32_fp8(va, 0) / sci) * (__builtin_amdgcn_cvt_f32_fp8(vb, 0) / scp);
       } else {
         dot += to_f32<Tc>(a) * to_f32<Tc>(b);
       }
     }
   }
   for (int e = d + threadIdx.x; e < dk; e += 256) { zi[e] = from_f32<Tc>(0.f); zp[e] = from_f32<Tc>(0.f); }
-  if constexpr (Q8)
+  if constexpr (Q8) {
     for (int e = d + threadIdx.x; e < dk8; e += 256) { zi8[e] = 0; zp8[e] = 0; }
+    if (threadIdx.x == 0) {  // E8M0 scale byte right after the row's K range (see Geometry::ld_k8)
+      zi8[dk8] = (unsigned char)(127 - ei);
+      zp8[dk8] = (unsigned char)(127 - ep);
+    }
+  }
   dot = block_sum(dot, red);
   if (threadIdx.x == 0) {
     inv[i] = ivi; inv[pi] = ivp;
@@ -216,6 +233,18 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
   ssp = wave_sum(ssp);
   const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
   const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  // fp8: per-row power-of-two scale from the row's amax (amax of z = amax of h * inv exactly)
+  int ei = 0, ep = 0;
+  if constexpr (Q8) {
+    float mxi = 0.f, mxp = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { mxi = fmaxf(mxi, fabsf(a[c][j])); mxp = fmaxf(mxp, fabsf(b[c][j])); }
+    ei = fp8_row_exp(xrow_max(row16_max(mxi)) * ivi);
+    ep = fp8_row_exp(xrow_max(row16_max(mxp)) * ivp);
+  }
+  const float sci = __int_as_float((ei + 127) << 23), scp = __int_as_float((ep + 127) << 23);
   float dot = 0.f;
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
@@ -227,16 +256,21 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
       store8<Tc>(zi + e, a[c], qa);
       store8<Tc>(zp + e, b[c], qb);
       if constexpr (Q8) {
-        *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa);
-        *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb);
+        *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa, sci);
+        *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb, scp);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) dot += qa[j] * qb[j];
     }
   }
   for (int e = d + lane; e < dk; e += 64) { zi[e] = from_f32<Tc>(0.f); zp[e] = from_f32<Tc>(0.f); }
-  if constexpr (Q8)
+  if constexpr (Q8) {
     for (int e = d + lane; e < dk8; e += 64) { zq8[(long long)i * ldk8 + e] = 0; zq8[(long long)pi * ldk8 + e] = 0; }
+    if (lane == 0) {  // E8M0 scale byte right after the row's K range (see Geometry::ld_k8)
+      zq8[(long long)i * ldk8 + dk8] = (unsigned char)(127 - ei);
+      zq8[(long long)pi * ldk8 + dk8] = (unsigned char)(127 - ep);
+    }
+  }
   dot = wave_sum(dot);
   if (lane == 0) {
     inv[i] = ivi; inv[pi] = ivp;
@@ -464,12 +498,12 @@ void dispatch_gemm(DType t, F&& f) {
 }
 
 // fp8 forward GEMMs: accumulators are products of e4m3(z * 256) values.
-void set_operand_scales(dev::SimParams& p, DType comp) {
-  if (comp == DType::FP8) {
-    const float inv2 = 1.0f / (dev::kFp8Scale * dev::kFp8Scale);
-    p.acc_scale = p.y_scale * inv2;
-    p.cos_scale = inv2;
-  }
+// fp8 forward GEMMs: the block-scaled MFMA applies each row's E8M0 scale (stored right after
+// the row's dim_k8 bytes), so accumulators are unscaled dot products like the other dtypes.
+void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
+  p.acc_scale = p.y_scale;
+  p.cos_scale = 1.0f;
+  p.scale_off = comp == DType::FP8 ? g.dim_k8 : 0;
 }
 
 // Diagnostic builds (-DNTXENT_ABLATION_KERNELS) pick a compile-time ablation of the GEMM
@@ -489,13 +523,20 @@ int gemm_ablation() {
 template <typename Tc, int MODE>
 void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
 #ifdef NTXENT_ABLATION_KERNELS
-  if constexpr (std::is_same<Tc, _Float16>::value) switch (gemm_ablation()) {
+  if constexpr (std::is_same<Tc, _Float16>::value || std::is_same<Tc, dev::fp8e4m3>::value) switch (gemm_ablation()) {
+    // fp8: only the timeline build (64) is instantiated
 #define NTXENT_ABL_CASE(A) \
-    case A: hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); return;
+    case A:                                                                                                  \
+      if constexpr (std::is_same<Tc, _Float16>::value) {                                                    \
+        hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); \
+        return;                                                                                              \
+      }                                                                                                      \
+      break;
     NTXENT_ABL_CASE(1) NTXENT_ABL_CASE(2) NTXENT_ABL_CASE(3) NTXENT_ABL_CASE(4) NTXENT_ABL_CASE(5)
     NTXENT_ABL_CASE(6) NTXENT_ABL_CASE(14) NTXENT_ABL_CASE(22) NTXENT_ABL_CASE(30)
 #undef NTXENT_ABL_CASE
     case 32: {  // clock stamps of block 0 (waves 0 and 4), dumped to stderr (synchronising)
+      if constexpr (!std::is_same<Tc, _Float16>::value) break;
       static unsigned long long* buf = nullptr;
       if (!buf) NTXENT_HIP_CHECK(hipMalloc(&buf, 512 * 8));
       NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, 512 * 8, stream));
@@ -617,7 +658,8 @@ size_t sk_counter_bytes(int num_cus) { return ((size_t)2 * std::max(1, num_cus) 
 int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipStream_t stream) {
   NTXENT_CHECK(p.kbytes % kKStepBytes == 0, "K not aligned to the K step");
   const int nk = (int)(p.kbytes / kKStepBytes);
-  const GemmSchedule s = make_schedule(ntiles, nk, ws.num_cus);
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+  const GemmSchedule s = make_schedule(ntiles, nk, cus);
   p.nk = s.nk;
   p.dp_tiles = s.dp_tiles;
   p.sk_tiles = s.sk_tiles;
@@ -670,7 +712,7 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
   g.ld_k = padded_ld(g.dim_k);
   g.ld_t = padded_ld(g.rows_pad);
   g.dim_k8 = roundup(dim, 128);
-  g.ld_k8 = padded_ld(g.dim_k8);
+  g.ld_k8 = g.dim_k8 + 64;  // >= 1 spare byte per row for the E8M0 row scale; never a 1 KiB multiple
   g.world = world;
   g.rank = rank;
   g.row_tiles = g.rows_pad / kTile;
@@ -862,7 +904,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
   const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
-  set_operand_scales(p, comp);
+  set_operand_scales(p, comp, g);
   p.A = rowmajor_operand(zq_local, ld, kb);
   p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;
@@ -887,7 +929,7 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
   const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
-  set_operand_scales(p, comp);
+  set_operand_scales(p, comp, g);
   p.A = rowmajor_operand(zq_local, ld, kb);
   p.B = rowmajor_operand(zq_all, ld, kb);
   p.tiles = tiles;

@@ -55,8 +55,9 @@ struct SimParams {
   int b_tile0;           // B operand: global column tile of the chunk's first row tile (ring mode)
   int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
-  float acc_scale;       // logit (log2 units) per accumulator unit: y_scale, / kFp8Scale^2 for fp8
-  float cos_scale;       // cosine per accumulator unit: 1, or 1 / kFp8Scale^2 for fp8
+  float acc_scale;       // logit (log2 units) per accumulator unit (y_scale)
+  float cos_scale;       // cosine per accumulator unit (1)
+  int scale_off;         // fp8 operands: byte offset of each row's E8M0 scale (= K bytes of a row)
   int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
   char* sc;              // kept cosines: [n_fwd_tiles][256*256] (canonical fragment order)
@@ -234,6 +235,14 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
 }
 
+// Block-scaled fp8 MFMA with the scale bytes selected by op_sel: byte IA of sa, byte IB of sb
+// (the builtin's op_sel operands must be literals).
+template <int IA, int IB>
+__device__ __forceinline__ f32x4 mma_mx_c(const i32x8& a, const i32x8& b, f32x4 c, int sa, int sb) {
+  // cbsz = blgp = 0: both operands fp8 e4m3
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, IA, sa, IB, sb);
+}
+
 // ------------------------------------------------------------------------------------
 // The similarity GEMM with its three epilogues (see the file header for the schedule).
 // ------------------------------------------------------------------------------------
@@ -283,13 +292,23 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   };
 
   f32x4 acc[8][4];
+  constexpr bool kF8 = std::is_same<T, fp8e4m3>::value;
+  // fp8: E8M0 scales of this lane's 8 A rows (sa_pk[h] byte mi: row 128 h + 64 wa + 16 mi + r16)
+  // and 4 B rows (sb_pk byte 2 qb + ni: row 128 qb + 32 wb + 16 ni + r16), loaded per tile
+  int sa_pk[2] = {0, 0}, sb_pk = 0;
 
   const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
-  frag af[2][4], bf0[2][2], bf1[2][2];  // [k-substep][block]
-  auto read_a = [&](int buf, int h, frag (&af)[2][4]) {
+  // Operand registers [k-substep][block]. fp8: ONE 32-byte register set per block holding both
+  // k-substeps (.lo = s 0, .hi = s 1), loaded in place so the block-scaled MFMA reads them
+  // without copies.
+  typedef typename std::conditional<kF8, i32x8, frag>::type OP;
+  constexpr int NS = kF8 ? 1 : 2;
+  typedef __attribute__((address_space(3))) const i32x4 lds_i4;
+  OP af[NS][4], bf0[NS][2], bf1[NS][2];
+  auto read_a = [&](int buf, int h, OP (&af)[NS][4]) {
     if constexpr ((ABL & 2) != 0) {  // ablation: operands stay as they are, opaque to the compiler
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) asm volatile("" : "+v"(af[s][mi]));
       return;
@@ -299,14 +318,21 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     for (int s = 0; s < 2; ++s) {
       const int pch = ((4 * s + cq) ^ sw) << 4;
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-        af[s][mi] = *(lds_frag*)(As + (128 * h + 64 * wa + 16 * mi + r16) * kKStepBytes + pch);
+      for (int mi = 0; mi < 4; ++mi) {
+        const lds_char* src = As + (128 * h + 64 * wa + 16 * mi + r16) * kKStepBytes + pch;
+        if constexpr (kF8) {
+          if (s == 0) af[0][mi].lo = *(lds_i4*)src;
+          else af[0][mi].hi = *(lds_i4*)src;
+        } else {
+          af[s][mi] = *(lds_frag*)src;
+        }
+      }
     }
   };
-  auto read_b = [&](int buf, int h, frag (&bf)[2][2]) {
+  auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
     if constexpr ((ABL & 2) != 0) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int ni = 0; ni < 2; ++ni) asm volatile("" : "+v"(bf[s][ni]));
       return;
@@ -316,16 +342,24 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     for (int s = 0; s < 2; ++s) {
       const int pch = ((4 * s + cq) ^ sw) << 4;
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-        bf[s][ni] = *(lds_frag*)(Bs + (128 * h + 32 * wb + 16 * ni + r16) * kKStepBytes + pch);
+      for (int ni = 0; ni < 2; ++ni) {
+        const lds_char* src = Bs + (128 * h + 32 * wb + 16 * ni + r16) * kKStepBytes + pch;
+        if constexpr (kF8) {
+          if (s == 0) bf[0][ni].lo = *(lds_i4*)src;
+          else bf[0][ni].hi = *(lds_i4*)src;
+        } else {
+          bf[s][ni] = *(lds_frag*)src;
+        }
+      }
     }
   };
   // s_setprio(1)/(0) around each MFMA cluster keeps hipcc from sinking the cluster across the
   // next s_barrier (cdna_hip_programming.md §5.5 T5).
-  auto mma_quadrant = [&](int qa, int qb, frag (&af)[2][4], frag (&bf)[2][2]) {
+  auto mma_quadrant = [&](auto qa_c, auto qb_c, OP (&af)[NS][4], OP (&bf)[NS][2]) {
+    constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
     if constexpr ((ABL & 4) != 0) {  // ablation: consume the operands, issue no MFMA
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < NS; ++s) {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) asm volatile("" ::"v"(af[s][mi]));
 #pragma unroll
@@ -334,17 +368,40 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       return;
     }
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (kF8) {
+      // one block-scaled MFMA per (row block, column block) over the whole 128-element K-step;
+      // the row scales are byte mi of sa_pk[qa] and byte 2 qb + ni of sb_pk
+      static_assert(MODE != kModeDz, "fp8 operands are forward-only");
+      auto mx = [&](auto mi_c, auto ni_c) {  // op_sel (scale byte) must be a literal
+        constexpr int mi = decltype(mi_c)::value, ni = decltype(ni_c)::value;
+        f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
+        c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, sa_pk[qa], sb_pk);
+        // The block-scaled MFMA intrinsic is not convergent, so LLVM's IR sinking moved every
+        // cluster of a K-step into the loop latch (one 32-MFMA cluster, operands of all phases
+        // live at once -> spills and a vmcnt(0) in the loop). An empty asm use pins it here.
+        asm volatile("" ::"v"(c));
+      };
+      typedef std::integral_constant<int, 0> I0;
+      typedef std::integral_constant<int, 1> I1;
+      typedef std::integral_constant<int, 2> I2;
+      typedef std::integral_constant<int, 3> I3;
+      mx(I0{}, I0{}); mx(I0{}, I1{}); mx(I1{}, I0{}); mx(I1{}, I1{});
+      mx(I2{}, I0{}); mx(I2{}, I1{}); mx(I3{}, I0{}); mx(I3{}, I1{});
+    } else {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
-          c = (MODE == kModeDz) ? Mfma<T>::mma(bf[s][ni], af[s][mi], c) : Mfma<T>::mma(af[s][mi], bf[s][ni], c);
-        }
+          for (int ni = 0; ni < 2; ++ni) {
+            f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
+            c = (MODE == kModeDz) ? Mfma<T>::mma(bf[s][ni], af[s][mi], c) : Mfma<T>::mma(af[s][mi], bf[s][ni], c);
+          }
+    }
     __builtin_amdgcn_s_setprio(0);
   };
+  const std::integral_constant<int, 0> kI0{};
+  const std::integral_constant<int, 1> kI1{};
   int n_stamp = 0;  // ABL & 32: clock stamp after every barrier of K-steps [4, 12), block 0
   const bool stamper = (ABL & 32) && bid == 0 && lane == 0 && (w == 0 || w == 4);
   auto barrier = [&]() {
@@ -433,6 +490,21 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   tstamp(6 + 6 * item);
   Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
   Bb = p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride;
+  if constexpr (kF8) {
+    const unsigned char* As8 = reinterpret_cast<const unsigned char*>(Ab) + p.scale_off;
+    const unsigned char* Bs8 = reinterpret_cast<const unsigned char*>(Bb) + p.scale_off;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      unsigned v = 0;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) v |= (unsigned)As8[(128 * h + 64 * wa + 16 * mi + r16) * p.A.ld] << (8 * mi);
+      sa_pk[h] = (int)v;
+    }
+    unsigned v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v |= (unsigned)Bs8[(128 * (j >> 1) + 32 * wb + 16 * (j & 1) + r16) * p.B.ld] << (8 * j);
+    sb_pk = (int)v;
+  }
   {
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(k0, p.A, nsteps); sa1.init(k0, p.A, nsteps);
@@ -459,21 +531,21 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     stage(0, 1, sa1, nxt);          //   A1 of step ks+1
     a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
     lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
-    mma_quadrant(0, 0, af, bf0);
+    mma_quadrant(kI0, kI0, af, bf0);
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
     read_b(cur, 1, bf1);
     stage(0, 0, sa0, cur);          //   A0 of step ks+2
     barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
-    mma_quadrant(0, 1, af, bf1);
+    mma_quadrant(kI0, kI1, af, bf1);
     barrier();                      // phase 3 L
     read_a(cur, 1, af);
     stage(1, 0, sb0, cur);          //   B0 of step ks+2
     barrier(); lds_drain();         // phase 3 C (A1 is restaged two phases later)
-    mma_quadrant(1, 0, af, bf0);
+    mma_quadrant(kI1, kI0, af, bf0);
     dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
     barrier();                      // phase 4 C
-    mma_quadrant(1, 1, af, bf1);
+    mma_quadrant(kI1, kI1, af, bf1);
   }
   if (grp == 0) barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches

@@ -17,6 +17,7 @@
 
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <tuple>
@@ -174,9 +175,16 @@ static at::Tensor skewed_empty(at::IntArrayRef sizes, const at::TensorOptions& o
   return at::empty({numel + skew}, o).narrow(0, skew, numel).view(sizes);
 }
 
+// CUs left free for communication kernels by the GEMMs launched while it is non-zero (the
+// data-parallel paths set it around launches that overlap an RCCL transfer; see
+// parallel/commstats.py:comm_overlap).
+static std::atomic<int> g_grid_reserve{0};
+int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
+
 static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
   GemmWorkspace ws;
   ws.num_cus = P.num_cus;
+  ws.sched_cus = std::max(1, P.num_cus - std::min(g_grid_reserve.load(), P.num_cus / 2));
   ws.bytes = gemm_workspace_bytes(ntiles, P.num_cus);
   ws.ptr = device_scratch(like, ws.bytes, 0).data_ptr();
   return ws;
@@ -821,6 +829,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);
+  m.def("set_grid_reserve", &set_grid_reserve, py::arg("cus"),
+        "CUs the next similarity-GEMM launches leave free (for overlapped RCCL kernels); returns the old value");
   m.def("set_small_path", &set_small_path, py::arg("on"));
   m.def("small_path_enabled", &small_path_enabled);
   m.def("set_small_splits", &set_small_splits, py::arg("n"));

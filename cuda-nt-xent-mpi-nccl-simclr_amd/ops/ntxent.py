@@ -74,7 +74,7 @@ def ntxent_loss(h: torch.Tensor, temperature: float = 0.07, *, use_mixed_precisi
       temperature: tau.
       use_mixed_precision: fp32 inputs are computed in fp16 (fp32 accumulate) if True.
       compute: override the compute dtype: ``auto|fp32|fp16|bf16|fp8``. ``fp8`` runs the forward
-        similarity GEMM on e4m3 MFMA (per-tensor scale 256) and the backward in fp16; the
+        similarity GEMM on block-scaled e4m3 MFMA (per-row amax power-of-two scales) and the backward in fp16; the
         loss is that of the fp8-quantised rows (logit error ~1e-2 at tau=0.07, see
         tests/test_gpu_fp8.py).
       keep_logits: keep the cosine tiles (compute dtype) between forward and backward

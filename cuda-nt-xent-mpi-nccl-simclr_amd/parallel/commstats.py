@@ -60,3 +60,34 @@ def collect(reset: bool = True) -> Dict[str, float]:
     if reset:
         _spans.clear()
     return dict(out)
+
+
+def comm_reserve_cus(backend: str = "nccl") -> int:
+    """CUs a GEMM leaves free while an RCCL transfer it overlaps is in flight.
+
+    The similarity GEMMs are persistent (one 512-thread block per CU holding 128 KiB of LDS and
+    the whole register file), so without a reserve the RCCL kernels of an overlapped P2P /
+    all-gather cannot be scheduled until the GEMM ends. ``NTXENT_COMM_RESERVE_CUS`` overrides
+    the default of 8 (one per XCD: 3 % of the chip); gloo transfers are host-staged and complete
+    before the GEMM is launched, so they reserve nothing."""
+    if backend == "gloo":
+        return 0
+    import os
+
+    return max(0, int(os.environ.get("NTXENT_COMM_RESERVE_CUS", "8")))
+
+
+@contextlib.contextmanager
+def comm_overlap(cus: int):
+    """GEMMs launched inside the block leave ``cus`` CUs free (see :func:`comm_reserve_cus`)."""
+    if cus <= 0:
+        yield
+        return
+    from ..ops import _ext
+
+    C = _ext.load()
+    old = C.set_grid_reserve(int(cus))
+    try:
+        yield
+    finally:
+        C.set_grid_reserve(old)

@@ -29,7 +29,7 @@ import torch.distributed as dist
 
 from ..ops import _ext
 from ..ops.ntxent import resolve_compute
-from .commstats import span
+from .commstats import comm_overlap, comm_reserve_cus, span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 _TILE_CACHE: Dict[tuple, Dict[int, torch.Tensor]] = {}
@@ -84,7 +84,8 @@ def _ring(zq: torch.Tensor, group, fn):
         if s < W - 1:
             nxt = bufs[s % 2]
             works = _exchange(cur, nxt, group)
-        fn(q, cur)
+        with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if works else 0):
+            fn(q, cur)
         with span("ring_rows"):
             for w in works:
                 w.wait()

@@ -40,7 +40,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
-from .commstats import span
+from .commstats import comm_overlap, comm_reserve_cus, span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 Job = Tuple[int, int, int, int, int]  # (q, m0, m1, k0, k1): my row tiles [m0,m1) x q's row tiles [k0,k1)
@@ -199,12 +199,18 @@ class SymNTXentFunction(torch.autograd.Function):
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=dev)
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
-        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)  # overlaps chunk 0
-        for ws, (first, count) in zip(works, sym_chunk_segments(plan, jobs, nch)):
+        reserve = comm_reserve_cus(dist.get_backend(group))
+        with comm_overlap(reserve):  # chunk 0 of the rows is on the wire
+            C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)
+        segs = sym_chunk_segments(plan, jobs, nch)
+        for c, (ws, (first, count)) in enumerate(zip(works, segs)):
             with span("fwd_rows"):
                 for w in ws:
                     w.wait()
-            C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
+            # the next chunk (or the fp16 rows of an fp8 plan) is still on the wire
+            more = c + 1 < len(works) and bool(works[c + 1]) or bool(works_f16)
+            with comm_overlap(reserve if more else 0):
+                C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
         with span("fwd_rows"):
             for w in works_f16:
                 w.wait()
@@ -348,7 +354,8 @@ def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc
     contrib = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
     own, recv, views = sym_grad_slabs(plan, W, r, h.device)
     works = _p2p([(t, q) for q, t in contrib.items()], [(v, p) for p, v in views.items()], group)
-    sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
+    with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if works else 0):
+        sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
     with span("bwd_partner_grads"):
         for w in works:
             w.wait()

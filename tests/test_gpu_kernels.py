@@ -48,6 +48,8 @@ def _check(h_dev, T, compute, keep=True):
     assert abs(loss.item() - lref) <= lt * max(1.0, abs(lref)), (loss.item(), lref)
     err = (g.double().cpu() - gref).abs().max().item()
     scale = gref.abs().max().item()
+    print(f"PARITY rows={h_dev.shape[0]} dim={h_dev.shape[1]} in={h_dev.dtype} compute={compute} T={T} "
+          f"loss_rel_err={abs(loss.item() - lref) / max(1.0, abs(lref)):.3e} grad_rel_err={err / scale:.3e}")
     assert err <= gt * scale, (err, scale)
     return loss.item(), lref, err / scale
 

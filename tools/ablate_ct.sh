@@ -10,7 +10,7 @@ if [ "$1" = "build" ]; then
   mkdir -p $ROOT/build/abl
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -fPIC -O3 -DNTXENT_ABLATION_KERNELS -I$INC \
     -c $ROOT/cuda-nt-xent-mpi-nccl-simclr_amd/csrc/kernels/ntxent_kernels.hip -o $ROOT/build/abl/k.o || exit 1
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 $ROOT/build/ntxent_bench.o $ROOT/build/abl/k.o $ROOT/build/engine.o \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 $ROOT/build/ntxent_bench.o $ROOT/build/abl/k.o $ROOT/build/small_kernels.o $ROOT/build/engine.o \
     $ROOT/build/rccl_comm.o $ROOT/build/trace.o -o $ROOT/build/bin/ntxent_bench_abl -L/opt/rocm/lib -lrccl -ldl \
     -Wl,-rpath,/opt/rocm/lib || exit 1
   echo built
