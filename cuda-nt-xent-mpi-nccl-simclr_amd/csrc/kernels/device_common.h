@@ -86,6 +86,9 @@ template <> struct Mfma<fp8e4m3> {
 template <typename T> struct StoreT { typedef T type; };
 template <> struct StoreT<fp8e4m3> { typedef _Float16 type; };
 
+// E8M0 byte -> 2^(byte - 127) as fp32 (bytes 1..254: normal powers of two).
+__device__ __forceinline__ float e8m0_to_f32(unsigned char b) { return __int_as_float((int)b << 23); }
+
 // Per-row fp8 scale exponent: the largest e with amax * 2^e <= 448 (e4m3 max), clamped to
 // [0, 126]; the row's E8M0 scale byte is 127 - e. amax = 0 (a zero / pad row) gives e = 126.
 __device__ __forceinline__ int fp8_row_exp(float amax) {

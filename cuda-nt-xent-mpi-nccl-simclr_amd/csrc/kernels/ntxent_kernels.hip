@@ -527,7 +527,7 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
     // fp8: only the timeline build (64) is instantiated
 #define NTXENT_ABL_CASE(A) \
     case A:                                                                                                  \
-      if constexpr (std::is_same<Tc, _Float16>::value) {                                                    \
+      if constexpr (std::is_same<Tc, _Float16>::value || (A == 1 && std::is_same<Tc, dev::fp8e4m3>::value)) { \
         hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); \
         return;                                                                                              \
       }                                                                                                      \
@@ -536,7 +536,7 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
     NTXENT_ABL_CASE(6) NTXENT_ABL_CASE(14) NTXENT_ABL_CASE(22) NTXENT_ABL_CASE(30)
 #undef NTXENT_ABL_CASE
     case 32: {  // clock stamps of block 0 (waves 0 and 4), dumped to stderr (synchronising)
-      if constexpr (!std::is_same<Tc, _Float16>::value) break;
+
       static unsigned long long* buf = nullptr;
       if (!buf) NTXENT_HIP_CHECK(hipMalloc(&buf, 512 * 8));
       NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, 512 * 8, stream));

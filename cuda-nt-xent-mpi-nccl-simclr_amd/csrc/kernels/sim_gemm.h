@@ -255,7 +255,10 @@ template <typename T, int MODE, int ABL = 0, int FX = 1>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[MODE == kModeCoef ? kCoefLds : kGemmLds];
+  // fp8: 2 KiB more hold the dwords carrying the tile's 256 A-row and 256 B-row E8M0 scales (one
+  // array: a second __shared__ object makes hipcc drain the LDS-DMA before every ds_read)
+  constexpr int kScaleLds = MODE == kModeCoef ? kCoefLds : kGemmLds;
+  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + (std::is_same<T, fp8e4m3>::value ? 2048 : 0)];
   lds_char* lds = (lds_char*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -293,9 +296,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   f32x4 acc[8][4];
   constexpr bool kF8 = std::is_same<T, fp8e4m3>::value;
-  // fp8: E8M0 scales of this lane's 8 A rows (sa_pk[h] byte mi: row 128 h + 64 wa + 16 mi + r16)
-  // and 4 B rows (sb_pk byte 2 qb + ni: row 128 qb + 32 wb + 16 ni + r16), loaded per tile
-  int sa_pk[2] = {0, 0}, sb_pk = 0;
+  // fp8: the MFMA runs with unit E8M0 scales (127); the rows' power-of-two scales are applied to
+  // the accumulators before the epilogue (exact). Per-lane scale operands loaded per tile cost a
+  // vmcnt(0) drain of the prologue DMA (a plain load's first use with LDS-DMA in flight).
+  const int kUnitScale = 0x7f7f7f7f;
 
   const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
   // Operand registers [k-substep][block]. fp8: ONE 32-byte register set per block holding both
@@ -369,13 +373,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
     __builtin_amdgcn_s_setprio(1);
     if constexpr (kF8) {
-      // one block-scaled MFMA per (row block, column block) over the whole 128-element K-step;
-      // the row scales are byte mi of sa_pk[qa] and byte 2 qb + ni of sb_pk
+      // one block-scaled MFMA per (row block, column block) over the whole 128-element K-step
       static_assert(MODE != kModeDz, "fp8 operands are forward-only");
       auto mx = [&](auto mi_c, auto ni_c) {  // op_sel (scale byte) must be a literal
         constexpr int mi = decltype(mi_c)::value, ni = decltype(ni_c)::value;
         f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
-        c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, sa_pk[qa], sb_pk);
+        c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, kUnitScale, kUnitScale);
         // The block-scaled MFMA intrinsic is not convergent, so LLVM's IR sinking moved every
         // cluster of a K-step into the loop latch (one 32-MFMA cluster, operands of all phases
         // live at once -> spills and a vmcnt(0) in the loop). An empty asm use pins it here.
@@ -490,21 +493,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   tstamp(6 + 6 * item);
   Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
   Bb = p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride;
-  if constexpr (kF8) {
-    const unsigned char* As8 = reinterpret_cast<const unsigned char*>(Ab) + p.scale_off;
-    const unsigned char* Bs8 = reinterpret_cast<const unsigned char*>(Bb) + p.scale_off;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      unsigned v = 0;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) v |= (unsigned)As8[(128 * h + 64 * wa + 16 * mi + r16) * p.A.ld] << (8 * mi);
-      sa_pk[h] = (int)v;
-    }
-    unsigned v = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v |= (unsigned)Bs8[(128 * (j >> 1) + 32 * wb + 16 * (j & 1) + r16) * p.B.ld] << (8 * j);
-    sb_pk = (int)v;
-  }
   {
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(k0, p.A, nsteps); sa1.init(k0, p.A, nsteps);
@@ -517,6 +505,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   // prologue: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1 (the stream clamps keep the
   // trailing prefetches in bounds, so every wait count below is uniform)
+  if constexpr (kF8) {
+    // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
+    // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a 4-byte
+    // LDS-DMA issued before the half-tiles: the vmcnt(10) below retires it with A0(0), B0(0)
+    const int t = threadIdx.x;
+    const char* src = (t < 256 ? Ab + (long long)t * p.A.ld : Bb + (long long)(t - 256) * p.B.ld) + p.scale_off;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kScaleLds + 256 * w), 4, 0, 0);
+  }
   stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
   stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
@@ -632,6 +628,27 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   }
   tstamp(8 + 6 * item);
+
+  if constexpr (kF8) {
+    // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact (acc row = rb + 4 (lane >> 4) + r: four
+    // consecutive scale dwords; column = cb + (lane & 15))
+    typedef __attribute__((address_space(3))) const unsigned lds_u32;
+    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+    float cf[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      cf[ni] = e8m0_to_f32((unsigned char)*(lds_u32*)(lds + kScaleLds + 4 * (256 + cb[ni] + (lane & 15))));
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const u32x4 e4 = *(lds_u32x4*)(lds + kScaleLds + 4 * (rb[mi] + 4 * (lane >> 4)));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float rf = e8m0_to_f32((unsigned char)e4[r]);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni][r] *= rf * cf[ni];
+      }
+    }
+  }
 
   if (p.dbg & kDbgNoEpilogue) {  // timing ablation: keep the MFMA results live, write nothing
     float s = 0.f;

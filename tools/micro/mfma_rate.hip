@@ -40,17 +40,25 @@ int main() {
   for (int i = 0; i < 1024; ++i) h[i] = (i * 2654435761u) & 0x3f3f3f3f;  // small finite fp8/fp16 patterns
   hipMemcpy(in, h, 4096, hipMemcpyHostToDevice);
   const int iters = 4096;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0); hipEventCreate(&e1);
   const char* names[3] = {"f16 16x16x32", "mx fp8 16x16x128 scale=127", "mx fp8 16x16x128 per-lane scales"};
   for (int m = 0; m < 3; ++m) {
+    float ms = 0;
     for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0, 0);
       if (m == 0) hipLaunchKernelGGL(k<0>, dim3(256), dim3(256), 0, 0, in, out, cyc, iters);
       if (m == 1) hipLaunchKernelGGL(k<1>, dim3(256), dim3(256), 0, 0, in, out, cyc, iters);
       if (m == 2) hipLaunchKernelGGL(k<2>, dim3(256), dim3(256), 0, 0, in, out, cyc, iters);
+      hipEventRecord(e1, 0);
       hipDeviceSynchronize();
+      hipEventElapsedTime(&ms, e0, e1);
     }
+    const double flop = 256.0 * 4 * iters * 8 * (m == 0 ? 16384.0 : 65536.0);
     unsigned long long c;
     hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-    printf("%-36s %.1f cycles per MFMA (s_memtime ticks)\n", names[m], (double)c / (iters * 8.0));
+    printf("%-36s %.1f s_memtime ticks per MFMA, %.3f ms, %.1f TFLOP/s (1 wave per SIMD, all CUs)\n", names[m],
+           (double)c / (iters * 8.0), ms, flop / (ms * 1e-3) / 1e12);
   }
   return 0;
 }
