@@ -6,7 +6,10 @@
 //
 //   all_gather   normalised rows Zq / ZqT (32 MiB per rank at B=4096, d=2048, fp16) and the
 //                per-row LSE (fp32, Rpad floats per rank);
-//   all_reduce   the scalar loss.
+//   all_reduce   the scalar loss;
+//   reduce_scatter / send_recv / all_gather_chunks   the gradient reduce-scatter, the grouped
+//                point-to-point exchanges of the symmetric data-parallel mode and chunked row
+//                gathers (consumers start on the chunks that have arrived).
 //
 // MI355X nodes are a full xGMI mesh (7 links x ~153 GB/s per GPU), so besides RCCL's own
 // all-gather (kRccl) there is a direct mesh variant (kMesh: every rank sends its shard to
@@ -20,10 +23,19 @@
 #include <cstddef>
 #include <memory>
 #include <string>
+#include <vector>
 
 namespace ntxent {
 
 enum class AllGatherAlgo : int { kRccl = 0, kMesh = 1 };
+
+// One side of a point-to-point transfer (see Comm::send_recv).
+struct P2POp {
+  bool send = true;     // true: send `bytes` from buf to peer; false: receive into buf from peer
+  void* buf = nullptr;
+  size_t bytes = 0;
+  int peer = 0;
+};
 
 // Collectives enqueued on a caller-provided stream (graph-capturable).
 class Comm {
@@ -35,6 +47,18 @@ class Comm {
   // send == recv + rank * bytes.
   virtual void all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) = 0;
   virtual void all_reduce_sum(float* buf, size_t count, hipStream_t stream) = 0;
+  // recv[count] = sum over ranks of send[rank * count .. (rank + 1) * count) (the backward
+  // "reduce-scatter of embedding grads" of the data-parallel NT-Xent).
+  virtual void reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) = 0;
+  // One grouped batch of point-to-point transfers: every peer's transfers run concurrently on its
+  // own xGMI link (RCCL: ncclGroupStart/End). Sends and receives between a pair match in order.
+  virtual void send_recv(const std::vector<P2POp>& ops, hipStream_t stream) = 0;
+  // all_gather in `nchunks` pieces of every rank's shard: piece c of all ranks (one grouped
+  // batch) lands before piece c + 1, and events[c] (optional, nchunks of them) is recorded on
+  // `stream` after piece c, so consumers can start on the rows that have arrived. In place as
+  // all_gather. Bytes are split on 256-byte boundaries.
+  void all_gather_chunks(const void* send, void* recv, size_t bytes, int nchunks, hipStream_t stream,
+                         hipEvent_t* events = nullptr);
   // Throws if an asynchronous communicator error was reported (RCCL: ncclCommGetAsyncError).
   virtual void check() {}
 };
@@ -46,6 +70,8 @@ class LocalComm final : public Comm {
   int world() const override { return 1; }
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) override;
   void all_reduce_sum(float*, size_t, hipStream_t) override {}
+  void reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) override;
+  void send_recv(const std::vector<P2POp>& ops, hipStream_t stream) override;  // peer 0 only: copies
 };
 
 // RCCL communicator (one per process / GPU).
@@ -63,6 +89,8 @@ class RcclComm final : public Comm {
   int world() const override { return world_; }
   void all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) override;
   void all_reduce_sum(float* buf, size_t count, hipStream_t stream) override;
+  void reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) override;
+  void send_recv(const std::vector<P2POp>& ops, hipStream_t stream) override;
   void check() override;
   void abort();  // tear the communicator down after an error (pending collectives fail)
   AllGatherAlgo algo() const { return algo_; }

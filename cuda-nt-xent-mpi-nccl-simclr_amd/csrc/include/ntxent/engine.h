@@ -43,6 +43,9 @@ struct EngineConfig {
   bool check_finite = false;  // loss() throws on a non-finite loss
   bool small_path = true;     // single-rank small problems: the one-launch fwd / bwd kernels
   int small_splits = 0;       // small path: backward column splits (0: small_bwd_splits)
+  // world > 1: CUs the similarity GEMMs leave free while an overlapped all-gather is in flight
+  // (the persistent GEMM would otherwise hold every CU and the RCCL kernels could not start)
+  int comm_reserve_cus = 8;
   int device = -1;            // -1: current device
 };
 

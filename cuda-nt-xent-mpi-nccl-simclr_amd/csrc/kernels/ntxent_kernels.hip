@@ -817,7 +817,10 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
     s.ipb = 0;
     return s;
   }
-  const int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
+  int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
+#ifdef NTXENT_ABLATION_KERNELS
+  if (const char* e = std::getenv("NTXENT_SK_SPLIT")) p_opt = std::max(1, std::atoi(e));  // diagnostic builds only
+#endif
   const int p = std::max(1, std::min({p_opt, G0 / rem, nk}));
   s.grid = q > 0 ? G0 : rem * p;
   s.ipb = (nk + p - 1) / p;  // K-steps per stream-K block; ceil(rem * nk / ipb) <= rem * p blocks busy

@@ -303,8 +303,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
   // Operand registers [k-substep][block]. fp8: ONE 32-byte register set per block holding both
-  // k-substeps (.lo = s 0, .hi = s 1), loaded in place so the block-scaled MFMA reads them
-  // without copies.
+  // k-substeps (low half = s 0, high half = s 1) for the block-scaled MFMA.
   typedef typename std::conditional<kF8, i32x8, frag>::type OP;
   constexpr int NS = kF8 ? 1 : 2;
   typedef __attribute__((address_space(3))) const i32x4 lds_i4;
@@ -318,6 +317,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       return;
     }
     const lds_char* As = lds + buf * kStageBytes;
+    i32x4 lo[4];  // fp8: k-substep 0, joined with substep 1 into a fully (re)defined operand (a
+                  // .lo/.hi partial write would keep the other half live across the whole kernel)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int pch = ((4 * s + cq) ^ sw) << 4;
@@ -325,8 +326,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       for (int mi = 0; mi < 4; ++mi) {
         const lds_char* src = As + (128 * h + 64 * wa + 16 * mi + r16) * kKStepBytes + pch;
         if constexpr (kF8) {
-          if (s == 0) af[0][mi].lo = *(lds_i4*)src;
-          else af[0][mi].hi = *(lds_i4*)src;
+          if (s == 0) lo[mi] = *(lds_i4*)src;
+          else af[0][mi] = __builtin_shufflevector(lo[mi], *(lds_i4*)src, 0, 1, 2, 3, 4, 5, 6, 7);
         } else {
           af[s][mi] = *(lds_frag*)src;
         }
@@ -342,6 +343,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       return;
     }
     const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
+    i32x4 lo[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int pch = ((4 * s + cq) ^ sw) << 4;
@@ -349,8 +351,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       for (int ni = 0; ni < 2; ++ni) {
         const lds_char* src = Bs + (128 * h + 32 * wb + 16 * ni + r16) * kKStepBytes + pch;
         if constexpr (kF8) {
-          if (s == 0) bf[0][ni].lo = *(lds_i4*)src;
-          else bf[0][ni].hi = *(lds_i4*)src;
+          if (s == 0) lo[ni] = *(lds_i4*)src;
+          else bf[0][ni] = __builtin_shufflevector(lo[ni], *(lds_i4*)src, 0, 1, 2, 3, 4, 5, 6, 7);
         } else {
           bf[s][ni] = *(lds_frag*)src;
         }
@@ -545,6 +547,27 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
   if (grp == 0) barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
+  if constexpr (kF8) {
+    // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact, before any stream-K sum (acc row = rb +
+    // 4 (lane >> 4) + r: four consecutive scale dwords; column = cb + (lane & 15))
+    typedef __attribute__((address_space(3))) const unsigned lds_u32;
+    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+    float cf[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      cf[ni] = e8m0_to_f32((unsigned char)*(lds_u32*)(lds + kScaleLds + 4 * (256 + 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1) + (lane & 15))));
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const u32x4 e4 = *(lds_u32x4*)(lds + kScaleLds + 4 * (128 * (mi >> 2) + 64 * wa + 16 * (mi & 3) + 4 * (lane >> 4)));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float rf = e8m0_to_f32((unsigned char)e4[r]);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni][r] *= rf * cf[ni];
+      }
+    }
+  }
+
   __syncthreads();
   tstamp(7 + 6 * item);
   {
@@ -609,46 +632,65 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     // The own segment stays in registers when it is the first or second term of the sum
     // ((s_b0 + s_me) = (s_me + s_b0) bitwise); a later position re-reads it from its slab.
     const bool reload_all = bid - b0 >= 2;
+    if constexpr (kF8) {
+      // (the pipelined form below made hipcc spill ~0.5 KiB per lane in the fp8 kernels)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      for (int bb = b0; bb <= b1; ++bb) {
-        if (bb == bid && !reload_all) continue;
-        const unsigned off = slot_off(bb) + lane_off;
+      for (int g = 0; g < 4; ++g) {
+        for (int bb = b0; bb <= b1; ++bb) {
+          if (bb == bid && !reload_all) continue;
+          const unsigned off = slot_off(bb) + lane_off;
+          u32x4 v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(off + (g * 8 + j) * 64 * 16), 0, 16);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
+            f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
+            a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
+          }
+        }
+      }
+    } else {
+      // Slab reads are software-pipelined: the next contributor's 8 loads are in flight while the
+      // current ones are added (one serial round trip per (g, slab) made the fixup of a tile split
+      // 7 ways ~14 us at d = 8192). The next index is clamped, not branched on, so no load is
+      // conditional (hipcc would wait vmcnt(0) around it).
+      auto next_bb = [&](int bb) {
+        int nb = bb + 1;
+        if (nb == bid && !reload_all) ++nb;
+        return nb;
+      };
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        int bb = (b0 == bid && !reload_all) ? b0 + 1 : b0;  // <= b1: the last arriver is never alone
         u32x4 v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(off + (g * 8 + j) * 64 * 16), 0, 16);
+          v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(slot_off(bb) + lane_off + (g * 8 + j) * 64 * 16), 0, 16);
+        for (;;) {
+          const int nb = next_bb(bb);
+          const bool more = nb <= b1;
+          const unsigned noff = slot_off(more ? nb : bb) + lane_off;
+          u32x4 nv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
-          f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
-          a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
+          for (int j = 0; j < 8; ++j)
+            nv[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(noff + (g * 8 + j) * 64 * 16), 0, 16);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
+            f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
+            a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
+          }
+          if (!more) break;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = nv[j];
+          bb = nb;
         }
       }
     }
   }
   tstamp(8 + 6 * item);
-
-  if constexpr (kF8) {
-    // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact (acc row = rb + 4 (lane >> 4) + r: four
-    // consecutive scale dwords; column = cb + (lane & 15))
-    typedef __attribute__((address_space(3))) const unsigned lds_u32;
-    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
-    float cf[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      cf[ni] = e8m0_to_f32((unsigned char)*(lds_u32*)(lds + kScaleLds + 4 * (256 + cb[ni] + (lane & 15))));
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const u32x4 e4 = *(lds_u32x4*)(lds + kScaleLds + 4 * (rb[mi] + 4 * (lane >> 4)));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float rf = e8m0_to_f32((unsigned char)e4[r]);
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni][r] *= rf * cf[ni];
-      }
-    }
-  }
 
   if (p.dbg & kDbgNoEpilogue) {  // timing ablation: keep the MFMA results live, write nothing
     float s = 0.f;

@@ -137,16 +137,19 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
     zqt_pending_ = true;
   }
+  // both forward launches overlap a gather (rows, then ZqT): leave CUs for the RCCL kernels
+  GemmWorkspace ws_ovl = ws_;
+  if (world_ > 1) ws_ovl.sched_cus = std::max(1, ws_.num_cus - std::min(cfg_.comm_reserve_cus, ws_.num_cus / 2));
   {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
-    launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_, g_, s);
+    launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s);
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");
     if (world_ > 1) NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zq_, 0));
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
-                     sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_, g_, s);
+                     sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_ovl, g_, s);
   }
   {
     NTXENT_TRACE("ntxent.lse");

@@ -1,6 +1,7 @@
 // RCCL implementation of ntxent::Comm (see include/ntxent/comm.h).
 #include "ntxent/comm.h"
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -11,6 +12,51 @@
 namespace ntxent {
 void LocalComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
   if (send != recv && bytes) NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, stream));
+}
+
+void LocalComm::reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) {
+  if (send != recv && count)
+    NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, count * sizeof(float), hipMemcpyDeviceToDevice, stream));
+}
+
+void LocalComm::send_recv(const std::vector<P2POp>& ops, hipStream_t stream) {
+  // world 1: the only peer is this rank; the k-th send feeds the k-th receive
+  std::vector<const P2POp*> sends, recvs;
+  for (const auto& o : ops) {
+    NTXENT_CHECK(o.peer == 0, "LocalComm::send_recv: peer out of range");
+    (o.send ? sends : recvs).push_back(&o);
+  }
+  NTXENT_CHECK(sends.size() == recvs.size(), "LocalComm::send_recv: unmatched send/receive");
+  for (size_t k = 0; k < sends.size(); ++k) {
+    NTXENT_CHECK(sends[k]->bytes == recvs[k]->bytes, "LocalComm::send_recv: size mismatch");
+    if (sends[k]->bytes && sends[k]->buf != recvs[k]->buf)
+      NTXENT_HIP_CHECK(hipMemcpyAsync(recvs[k]->buf, sends[k]->buf, sends[k]->bytes, hipMemcpyDeviceToDevice, stream));
+  }
+}
+
+void Comm::all_gather_chunks(const void* send, void* recv, size_t bytes, int nchunks, hipStream_t stream,
+                             hipEvent_t* events) {
+  NTXENT_CHECK(nchunks >= 1, "all_gather_chunks: nchunks must be >= 1");
+  const int W = world(), r = rank();
+  char* out = static_cast<char*>(recv);
+  const char* in = static_cast<const char*>(send);
+  char* own = out + (size_t)r * bytes;
+  const size_t unit = 256;
+  const size_t units = (bytes + unit - 1) / unit;
+  for (int c = 0; c < nchunks; ++c) {
+    const size_t b0 = std::min(bytes, units * c / nchunks * unit), b1 = std::min(bytes, units * (c + 1) / nchunks * unit);
+    if (b1 > b0) {
+      if (in != own) NTXENT_HIP_CHECK(hipMemcpyAsync(own + b0, in + b0, b1 - b0, hipMemcpyDeviceToDevice, stream));
+      std::vector<P2POp> ops;
+      for (int k = 1; k < W; ++k) {  // mesh: one link per peer, all in one group
+        const int to = (r + k) % W, from = (r - k + W) % W;
+        ops.push_back({true, own + b0, b1 - b0, to});
+        ops.push_back({false, out + (size_t)from * bytes + b0, b1 - b0, from});
+      }
+      if (!ops.empty()) send_recv(ops, stream);
+    }
+    if (events) NTXENT_HIP_CHECK(hipEventRecord(events[c], stream));
+  }
 }
 }  // namespace ntxent
 
@@ -25,6 +71,8 @@ RcclComm::RcclComm(int, int, const std::string&, int, AllGatherAlgo algo) : algo
 RcclComm::~RcclComm() = default;
 void RcclComm::all_gather(const void*, void*, size_t, hipStream_t) { no_rccl(); }
 void RcclComm::all_reduce_sum(float*, size_t, hipStream_t) { no_rccl(); }
+void RcclComm::reduce_scatter_sum(const float*, float*, size_t, hipStream_t) { no_rccl(); }
+void RcclComm::send_recv(const std::vector<P2POp>&, hipStream_t) { no_rccl(); }
 void RcclComm::check() {}
 void RcclComm::abort() {}
 }  // namespace ntxent
@@ -107,6 +155,32 @@ void RcclComm::all_reduce_sum(float* buf, size_t count, hipStream_t stream) {
   NTXENT_CHECK(!aborted_, "RcclComm: communicator aborted");
   if (world_ == 1) return;
   NTXENT_RCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+}
+
+void RcclComm::reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) {
+  NTXENT_TRACE("ntxent.reducescatter");
+  fault_point("reducescatter");
+  NTXENT_CHECK(!aborted_, "RcclComm: communicator aborted");
+  if (world_ == 1) {
+    if (send != recv && count)
+      NTXENT_HIP_CHECK(hipMemcpyAsync(recv, send, count * sizeof(float), hipMemcpyDeviceToDevice, stream));
+    return;
+  }
+  NTXENT_RCCL_CHECK(ncclReduceScatter(send, recv, count, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), stream));
+}
+
+void RcclComm::send_recv(const std::vector<P2POp>& ops, hipStream_t stream) {
+  NTXENT_TRACE("ntxent.sendrecv");
+  fault_point("sendrecv");
+  NTXENT_CHECK(!aborted_, "RcclComm: communicator aborted");
+  auto c = static_cast<ncclComm_t>(comm_);
+  NTXENT_RCCL_CHECK(ncclGroupStart());
+  for (const auto& o : ops) {
+    NTXENT_CHECK(o.peer >= 0 && o.peer < world_, "RcclComm::send_recv: peer out of range");
+    if (o.send) NTXENT_RCCL_CHECK(ncclSend(o.buf, o.bytes, ncclChar, o.peer, c, stream));
+    else NTXENT_RCCL_CHECK(ncclRecv(o.buf, o.bytes, ncclChar, o.peer, c, stream));
+  }
+  NTXENT_RCCL_CHECK(ncclGroupEnd());
 }
 
 void RcclComm::check() {

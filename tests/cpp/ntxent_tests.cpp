@@ -359,6 +359,67 @@ NT_TEST(RcclCommWorldOne) {
   comm.check();
 }
 
+// Comm extensions at world 1 (the multi-rank behaviour runs on the driver's 8-GPU node): the
+// reduce-scatter, the grouped point-to-point batch (self-exchange) and the chunked all-gather
+// with per-chunk events, for both the local and the RCCL communicator.
+static void comm_primitives(Comm& c, const char* name) {
+  hipStream_t s;
+  NTXENT_HIP_CHECK(hipStreamCreate(&s));
+  const size_t n = 1000, bytes = 3000 * 4 + 44;  // not a multiple of the 256-byte chunk unit
+  std::vector<float> hs(n);
+  for (size_t i = 0; i < n; ++i) hs[i] = 0.5f * (float)i - 7.f;
+  float *a = nullptr, *b = nullptr;
+  char *src = nullptr, *dst = nullptr;
+  NTXENT_HIP_CHECK(hipMalloc(&a, n * 4));
+  NTXENT_HIP_CHECK(hipMalloc(&b, n * 4));
+  NTXENT_HIP_CHECK(hipMalloc(&src, bytes));
+  NTXENT_HIP_CHECK(hipMalloc(&dst, bytes));
+  NTXENT_HIP_CHECK(hipMemcpy(a, hs.data(), n * 4, hipMemcpyHostToDevice));
+  c.reduce_scatter_sum(a, b, n, s);
+  std::vector<float> out(n);
+  NTXENT_HIP_CHECK(hipMemcpyAsync(out.data(), b, n * 4, hipMemcpyDeviceToHost, s));
+  NTXENT_HIP_CHECK(hipStreamSynchronize(s));
+  EXPECT(out == hs, "%s: reduce_scatter_sum at world 1 is not the identity", name);
+  // grouped self send/recv
+  NTXENT_HIP_CHECK(hipMemsetAsync(b, 0, n * 4, s));
+  c.send_recv({P2POp{true, a, n * 4, 0}, P2POp{false, b, n * 4, 0}}, s);
+  NTXENT_HIP_CHECK(hipMemcpyAsync(out.data(), b, n * 4, hipMemcpyDeviceToHost, s));
+  NTXENT_HIP_CHECK(hipStreamSynchronize(s));
+  EXPECT(out == hs, "%s: send_recv self-exchange", name);
+  // chunked all-gather, out of place and in place, with per-chunk events
+  std::vector<unsigned char> hb(bytes), ob(bytes);
+  for (size_t i = 0; i < bytes; ++i) hb[i] = (unsigned char)(i * 7 + 3);
+  NTXENT_HIP_CHECK(hipMemcpy(src, hb.data(), bytes, hipMemcpyHostToDevice));
+  hipEvent_t ev[3];
+  for (auto& e : ev) NTXENT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  NTXENT_HIP_CHECK(hipMemsetAsync(dst, 0, bytes, s));
+  c.all_gather_chunks(src, dst, bytes, 3, s, ev);
+  NTXENT_HIP_CHECK(hipEventSynchronize(ev[2]));
+  NTXENT_HIP_CHECK(hipMemcpy(ob.data(), dst, bytes, hipMemcpyDeviceToHost));
+  EXPECT(ob == hb, "%s: all_gather_chunks out of place", name);
+  c.all_gather_chunks(dst, dst, bytes, 5, s);
+  NTXENT_HIP_CHECK(hipStreamSynchronize(s));
+  NTXENT_HIP_CHECK(hipMemcpy(ob.data(), dst, bytes, hipMemcpyDeviceToHost));
+  EXPECT(ob == hb, "%s: all_gather_chunks in place", name);
+  for (auto& e : ev) NTXENT_HIP_CHECK(hipEventDestroy(e));
+  NTXENT_HIP_CHECK(hipFree(a));
+  NTXENT_HIP_CHECK(hipFree(b));
+  NTXENT_HIP_CHECK(hipFree(src));
+  NTXENT_HIP_CHECK(hipFree(dst));
+  NTXENT_HIP_CHECK(hipStreamDestroy(s));
+}
+
+NT_TEST(LocalCommPrimitives) {
+  LocalComm lc;
+  comm_primitives(lc, "LocalComm");
+}
+
+NT_TEST(RcclCommPrimitivesWorldOne) {
+  RcclComm comm(0, 1, RcclComm::unique_id(), 0);
+  comm_primitives(comm, "RcclComm");
+  comm.check();
+}
+
 NT_TEST(FaultInjection) {
   Harness hs(embeddings(128, 64, 14), 128, 64, DType::F32, DType::F32, kT, true, nullptr, /*check_finite=*/true);
   set_fault_sites("dz");
