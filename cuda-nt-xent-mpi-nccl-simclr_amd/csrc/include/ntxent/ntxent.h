@@ -116,10 +116,8 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
 // first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered.
 std::vector<int4> build_fwd_tiles(const Geometry& g);
 int count_own_fwd_tiles(const Geometry& g);
-// dZ tiles (ti, tn, ks, 0) for a split-K factor.
-std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit);
-// Split-K factor for the dZ GEMM; the stream-K schedule balances K itself, so this is 1.
-int choose_dz_ksplit(const Geometry& g, int num_cus);
+// dZ tiles (ti, tn, 0, 0): the persistent stream-K schedule balances K itself (no split-K).
+std::vector<int4> build_dz_tiles(const Geometry& g);
 
 // Persistent stream-K schedule of the similarity GEMMs: `grid` blocks first process
 // `dp_tiles` whole tiles in rounds, then split the K-steps of the remaining `sk_tiles` tiles
@@ -212,7 +210,7 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
                       const BlockView& bv = BlockView{});
 
 // dZ[Rpad][dim_n] = C * Z (fp32), C = the coefficient buffer, zqt_all = [W][dim_n][Rpad]
-// (all-gathered ZqT blocks); tiles from build_dz_tiles(g, 1).
+// (all-gathered ZqT blocks); tiles from build_dz_tiles(g).
 void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
                float* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
 
@@ -229,7 +227,7 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 // dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
 // xslabs (optional): nx more fp16 slabs [nx][Rpad][dim_n] added to the sum (received partner
 // contributions of the symmetric data-parallel mode).
-void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h,
+void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h,
                      const float* inv, const float* grad_out, void* dh, const Geometry& g,
                      hipStream_t stream, const void* xslabs = nullptr, int nx = 0);
 

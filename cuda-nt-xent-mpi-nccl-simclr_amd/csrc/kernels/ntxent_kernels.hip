@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
 // xs: nx extra fp16 slabs (received partner contributions, symmetric data-parallel mode) added
 // to the fp32 sum.
 template <typename Tin, int NCH>
-__global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int ksplit,
+__global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int nslabs,
                                                            long long slab_stride, long long ldo,
                                                            const Tin* __restrict__ h, const float* __restrict__ inv,
                                                            const float* __restrict__ grad_out, float alpha_base,
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
     if (e < d) {
       load8<Tin>(hi + e, z[c]);
       f32x4 a = *reinterpret_cast<const f32x4*>(gi + e), b = *reinterpret_cast<const f32x4*>(gi + e + 4);
-      for (int k = 1; k < ksplit; ++k) {
+      for (int k = 1; k < nslabs; ++k) {
         a += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e);
         b += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e + 4);
       }
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
 }
 
 template <typename Tin>
-__global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__ slabs, int ksplit,
+__global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__ slabs, int nslabs,
                                                        long long slab_stride, long long ldo,
                                                        const Tin* __restrict__ h, const float* __restrict__ inv,
                                                        const float* __restrict__ grad_out, float alpha_base,
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
   float dot = 0.f;
   for (int e = threadIdx.x; e < d; e += 256) {
     float g = 0.f;
-    for (int k = 0; k < ksplit; ++k) g += gi[k * slab_stride + e];
+    for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
     dot += to_f32<Tin>(hi[e]) * iv * g;
   }
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
   Tin* di = dh + (long long)i * d;
   for (int e = threadIdx.x; e < d; e += 256) {
     float g = 0.f;
-    for (int k = 0; k < ksplit; ++k) g += gi[k * slab_stride + e];
+    for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
     const float z = to_f32<Tin>(hi[e]) * iv;
     di[e] = from_f32<Tin>(alpha * iv * (g - z * dot));
@@ -641,11 +641,15 @@ dev::SimParams base_params(const Geometry& g) {
   p.acc_scale = p.y_scale;
   p.cos_scale = 1.0f;
   p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
-  static const int dbg = [] {
+#ifdef NTXENT_ABLATION_KERNELS
+  static const int dbg = [] {  // runtime epilogue/load ablations (diagnostic builds only)
     const char* e = std::getenv("NTXENT_GEMM_DEBUG");
     return e ? std::atoi(e) : 0;
   }();
   p.dbg = dbg;
+#else
+  p.dbg = 0;
+#endif
   return p;
 }
 
@@ -678,14 +682,7 @@ int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipSt
 
 // Leading dimension (elements) for a row of `n` elements: strides of a multiple of 1024
 // elements get 64 extra so the rows a tile streams rotate through the L2 channels.
-// NTXENT_LD_PAD overrides the pad (0 disables) for A/B measurements.
-int padded_ld(int n) {
-  static const int pad = [] {
-    const char* e = std::getenv("NTXENT_LD_PAD");
-    return e ? std::atoi(e) : 64;
-  }();
-  return (n % 1024 == 0) ? n + pad : n;
-}
+int padded_ld(int n) { return (n % 1024 == 0) ? n + 64 : n; }
 
 dev::OperandDesc rowmajor_operand(const void* base, long long ld_bytes, long long kbytes) {
   dev::OperandDesc o;
@@ -751,10 +748,8 @@ std::vector<int4> build_fwd_tiles(const Geometry& g) {
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int tj = 0; tj < g.col_tiles; ++tj)
       if (tj < own || tj >= own + g.row_tiles) tiles.push_back(make_int4(ti, tj, kTilePlain, 0));
-  if (std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1) {
-    zorder(tiles, 0, n_own);
-    zorder(tiles, n_own, tiles.size());
-  }
+  zorder(tiles, 0, n_own);
+  zorder(tiles, n_own, tiles.size());
   return tiles;
 }
 
@@ -764,8 +759,7 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int local = ti; local < g.row_tiles; ++local)
       tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
-  const bool z = std::getenv("NTXENT_TILE_ORDER") == nullptr || std::atoi(std::getenv("NTXENT_TILE_ORDER")) == 1;
-  if (z) zorder(tiles, 0, tiles.size());
+  zorder(tiles, 0, tiles.size());
   for (const SymJob& j : jobs) {
     NTXENT_CHECK(j.q >= 0 && j.q < g.world && j.q != g.rank, "sym job: bad partner");
     NTXENT_CHECK(0 <= j.m0 && j.m0 <= j.m1 && j.m1 <= g.row_tiles && 0 <= j.k0 && j.k0 <= j.k1 &&
@@ -781,20 +775,12 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
       for (int ti = j.m0; ti < j.m1; ++ti)
         for (int tj = std::max(j.k0, c0); tj < std::min(j.k1, c1); ++tj)
           tiles.push_back(make_int4(ti, j.q * g.row_tiles + tj, kTileCross, 0));
-    if (z) zorder(tiles, first, tiles.size());
+    zorder(tiles, first, tiles.size());
   }
   return tiles;
 }
 
 int count_own_fwd_tiles(const Geometry& g) { return g.row_tiles * (g.row_tiles + 1) / 2; }
-
-int choose_dz_ksplit(const Geometry& g, int num_cus) {
-  // The persistent stream-K schedule of every similarity GEMM balances K itself, so the dZ
-  // GEMM no longer needs a split-K factor (kept for API stability; always 1).
-  (void)g;
-  (void)num_cus;
-  return 1;
-}
 
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   // Whole tiles in data-parallel rounds of G = num_cus blocks; only the remainder tiles
@@ -837,12 +823,11 @@ size_t gemm_workspace_bytes(int ntiles, int num_cus) {
   return sk_counter_bytes(num_cus) + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float);
 }
 
-std::vector<int4> build_dz_tiles(const Geometry& g, int ksplit) {
+std::vector<int4> build_dz_tiles(const Geometry& g) {
   std::vector<int4> tiles;
   const int nt = g.dim_n / kTile;
   for (int ti = 0; ti < g.row_tiles; ++ti)
-    for (int ks = 0; ks < ksplit; ++ks)
-      for (int tn = 0; tn < nt; ++tn) tiles.push_back(make_int4(ti, tn, ks, 0));
+    for (int tn = 0; tn < nt; ++tn) tiles.push_back(make_int4(ti, tn, 0, 0));
   return tiles;
 }
 
@@ -1047,7 +1032,7 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h, const float* inv,
+void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h, const float* inv,
                      const float* grad_out, void* dh, const Geometry& g, hipStream_t stream,
                      const void* xslabs, int nx) {
   const _Float16* xs = static_cast<const _Float16*>(xslabs);
@@ -1061,16 +1046,16 @@ void launch_norm_bwd(DType in, const float* slabs, int ksplit, const void* h, co
     const Tin* hp = static_cast<const Tin*>(h);
     Tin* dp = static_cast<Tin*>(dh);
     if (vec && nch == 1)
-      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
                          ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec && nch == 2)
-      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
                          ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec)
-      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss,
+      hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
                          ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else
-      hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, ksplit, ss, ldo,
+      hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss, ldo,
                          hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
   });
   NTXENT_HIP_CHECK(hipGetLastError());

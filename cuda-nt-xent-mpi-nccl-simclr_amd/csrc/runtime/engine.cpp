@@ -40,7 +40,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   small_ = cfg.small_path && world_ == 1 && small_path_eligible(g_, cfg.compute);
 
   const auto ft = build_fwd_tiles(g_);
-  const auto dt = build_dz_tiles(g_, 1);
+  const auto dt = build_dz_tiles(g_);
   n_fwd_ = (int)ft.size();
   n_own_ = count_own_fwd_tiles(g_);
   n_dz_ = (int)dt.size();

@@ -63,7 +63,6 @@ struct Plan {
   int n_own = 0;  // own-rank tiles at the head of fwd_tiles
   at::Tensor dz_tiles;
   int n_dz = 0;
-  int ksplit = 1;
   int num_cus = 256;
   bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
 
@@ -110,8 +109,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->n_fwd = (int)ft.size();
   p->n_own = count_own_fwd_tiles(p->g);
   p->fwd_tiles = upload_tiles(ft, device);
-  p->ksplit = choose_dz_ksplit(p->g, di.num_cus);
-  auto dt = build_dz_tiles(p->g, p->ksplit);
+  auto dt = build_dz_tiles(p->g);
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
   p->small = small_path_eligible(p->g, comp);
@@ -148,33 +146,6 @@ static at::Tensor device_scratch(const at::Tensor& like, size_t bytes, int slot)
 }
 
 
-// Placement experiment (NTXENT_SKEW="zq,zqt,sc,cbuf,slabs" in KiB): start the named buffers
-// that many KiB into a slightly larger allocation. The caching allocator hands out large
-// blocks 2 MiB-aligned, so GEMM operands otherwise share their low address bits.
-static at::Tensor skewed_empty(at::IntArrayRef sizes, const at::TensorOptions& o, int slot) {
-  static const std::vector<long> kb = [] {
-    std::vector<long> v(5, 0);
-    if (const char* e = std::getenv("NTXENT_SKEW")) {
-      std::string str(e);
-      size_t pos = 0;
-      for (int i = 0; i < 5 && pos <= str.size(); ++i) {
-        const size_t c = str.find(',', pos);
-        v[i] = std::atol(str.substr(pos, c == std::string::npos ? std::string::npos : c - pos).c_str());
-        if (c == std::string::npos) break;
-        pos = c + 1;
-      }
-    }
-    return v;
-  }();
-  const long skew_b = (slot >= 0 && slot < 5) ? kb[slot] * 1024 : 0;
-  if (skew_b == 0) return at::empty(sizes, o);
-  long numel = 1;
-  for (auto d : sizes) numel *= d;
-  const long es = (long)c10::elementSize(c10::typeMetaToScalarType(o.dtype()));
-  const long skew = skew_b / es;
-  return at::empty({numel + skew}, o).narrow(0, skew, numel).view(sizes);
-}
-
 // CUs left free for communication kernels by the GEMMs launched while it is non-zero (the
 // data-parallel paths set it around launches that overlap an RCCL transfer; see
 // parallel/commstats.py:comm_overlap).
@@ -207,7 +178,7 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::opti
     NTXENT_CHECK(zq.numel() == (long)P.g.rows_pad * P.g.ld_k && zq.scalar_type() == to_scalar(P.bwd()),
                  "zq_out must be [rows_pad, ld_k] in the backward dtype");
   } else {
-    zq = skewed_empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())), 0);
+    zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())));
   }
   at::Tensor zq8;
   if (P.comp == DType::FP8) {
@@ -237,7 +208,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
     NTXENT_CHECK(zqt.numel() == (long)P.g.dim_n * P.g.ld_t && zqt.scalar_type() == zq.scalar_type(),
                  "zqt_out must be [dim_n, ld_t]");
   } else {
-    zqt = skewed_empty({P.g.dim_n, P.g.ld_t}, zq.options(), 1);
+    zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
   }
   launch_transpose(P.bwd(), zq.data_ptr(), zqt.data_ptr(), P.g, cur_stream(zq));
   return zqt;
@@ -252,7 +223,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos) sc = skewed_empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())), 2);
+  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -307,7 +278,7 @@ at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Te
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
-  auto cbuf = skewed_empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options(), 3);
+  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf));
   return cbuf;
@@ -317,7 +288,7 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
                      const at::Tensor& cpos, const Plan& P) {
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
-  auto cbuf = skewed_empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())), 3);
+  auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -330,7 +301,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
   const at::DeviceGuard guard(sc.device());
-  auto slabs = skewed_empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat), 4);
+  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
   auto ws = gemm_ws(sc, P.n_dz, P);
   launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, slabs.data_ptr<float>(), ws, P.g, cur_stream(sc));
@@ -343,7 +314,7 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
   const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
-  launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), P.ksplit, h.data_ptr(), inv.data_ptr<float>(),
+  launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
                   go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
   return dh;
 }
@@ -412,7 +383,7 @@ at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, c
   g1.world = 1;
   g1.rank = 0;
   g1.col_tiles = g1.row_tiles;
-  auto slabs = at::empty({P.ksplit, P.g.rows_pad, P.g.dim_n}, opts(cbuf_block, at::kFloat));
+  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(cbuf_block, at::kFloat));
   auto ws = gemm_ws(cbuf_block, P.n_dz, P);
   launch_dz(P.bwd(), cbuf_block.data_ptr(), zqt_chunk.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, slabs.data_ptr<float>(), ws, g1, cur_stream(cbuf_block));
@@ -605,19 +576,6 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
                      cur_stream(h));
     return {loss, pr[0], at::Tensor(), pr[1], lse2, at::Tensor(), arow};
   }
-  static const bool side_t = [] {
-    const char* e = std::getenv("NTXENT_SIDE_TRANSPOSE");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  if (!side_t) {
-    auto zqt = transpose(pr[0], *P, c10::nullopt);
-    const bool f8 = comp == DType::FP8;
-    auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
-    auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-    auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-    auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
-    return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
-  }
   // ZqT (the dZ GEMM's B operand) is first read in the backward: the transpose runs on a side
   // stream beside the forward GEMM, whose blocks (one per CU, 128 KiB LDS) leave LDS and
   // memory bandwidth for it, and the current stream joins it after the LSE kernel.
@@ -696,23 +654,41 @@ std::vector<at::Tensor> forward_with_stats(const at::Tensor& z, double T, bool u
 }
 
 // backward(z, stats, grad_out, T): the reference passes a softmax matrix here that its own
-// forward never returns (src/ntxent_kernel.cu:202). This op accepts anything in that slot and
-// recomputes the row statistics it needs (negatives-only LSE; cheap next to the backward
-// GEMMs), so results never depend on a possibly stale caller-provided softmax.
+// forward never returns (src/ntxent_kernel.cu:202). Here `stats` may be the per-row LSE that
+// forward_with_stats returns ([2N] fp32, natural log): the backward then costs ONE similarity
+// GEMM (the cosines are recomputed inside the coefficient GEMM; a stateless op keeps none).
+// Anything else in that slot (the reference's softmax, an empty tensor) is ignored and the row
+// statistics are recomputed (one more similarity GEMM), so results never depend on a stale
+// caller-provided softmax.
 // Returns (grad_z, grad_logits) where grad_logits = dL/dS is materialised only for 2N <= 4096.
 std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at::Tensor& stats,
                                                const at::Tensor& grad_out, double T, bool use_mixed_precision) {
-  (void)stats;
   auto z = z_in.contiguous();
   const at::DeviceGuard guard(z.device());
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
   auto pr = prep(z, *P, c10::nullopt, c10::nullopt);
   auto zqt = transpose(pr[0], *P, c10::nullopt);
-  auto lse2 = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
-  auto cpos = at::empty({P->g.rows_pad}, opts(z, at::kFloat));
-  auto fs = fwd_stats(pr[0], pr[0], *P, false);
-  lse(fs[0], pr[2], lse2, cpos, *P);
+  const long R = z.size(0), n = R / 2, Rp = P->g.rows_pad;
+  at::Tensor lse2, cpos;
+  const bool have_lse = stats.defined() && stats.dim() == 1 && stats.size(0) == R && stats.is_floating_point() &&
+                        stats.device() == z.device();
+  if (have_lse) {
+    // lse2 in log2 units; C_i,p(i) = -(a_i + a_p(i)), a_i = 1 - P_ip = -expm1(y_ip - lse_i)
+    // (expm1 keeps a_i accurate when P_ip -> 1)
+    auto lse_nat = stats.to(at::kFloat);
+    lse2 = at::zeros({Rp}, opts(z, at::kFloat));
+    lse2.narrow(0, 0, R).copy_(lse_nat * (float)1.4426950408889634);
+    auto y_nat = pr[2].narrow(0, 0, R) * (float)0.6931471805599453;
+    auto a = -at::expm1(y_nat - lse_nat);
+    cpos = at::zeros({Rp}, opts(z, at::kFloat));
+    cpos.narrow(0, 0, R).copy_(-(a + at::roll(a, {n})));
+  } else {
+    lse2 = at::empty({Rp}, opts(z, at::kFloat));
+    cpos = at::empty({Rp}, opts(z, at::kFloat));
+    auto fs = fwd_stats(pr[0], pr[0], *P, false);
+    lse(fs[0], pr[2], lse2, cpos, *P);
+  }
   auto sc = coef_gemm(pr[0], pr[0], lse2, cpos, *P);
   auto slabs = dz(sc, zqt, *P);
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
@@ -720,7 +696,6 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   at::Tensor grad_logits;
   if (z.size(0) <= 4096) {
     // dL/dS_ij = grad_out * (P_ij - [j == p(i)]) / 2N  (debug/parity output)
-    const long R = z.size(0), n = R / 2;
     auto zf = z.to(at::kFloat);
     auto zn = zf / zf.norm(2, {1}, true).clamp_min(1e-12);
     auto S = at::matmul(zn, zn.t()) / T;
@@ -791,7 +766,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_fwd_tiles", &Plan::n_fwd)
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
-      .def_readonly("ksplit", &Plan::ksplit)
       .def_readonly("small", &Plan::small)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
@@ -872,7 +846,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return tiles_to_list(ntxent::build_fwd_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f)));
   }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
   m.def("dz_tile_list", [tiles_to_list](int rows, int dim, int world, int rank) {
-    return tiles_to_list(ntxent::build_dz_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f), 1));
+    return tiles_to_list(ntxent::build_dz_tiles(ntxent::make_geometry(rows, dim, world, rank, 0.07f)));
   }, py::arg("rows"), py::arg("dim"), py::arg("world") = 1, py::arg("rank") = 0);
   m.def("sym_fwd_tile_list", [tiles_to_list](int rows, int dim, int world, int rank,
                                              const std::vector<std::tuple<int, int, int, int, int>>& jobs, int nchunks) {

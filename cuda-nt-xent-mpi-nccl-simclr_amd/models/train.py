@@ -9,6 +9,7 @@ from __future__ import annotations
 import argparse
 import dataclasses
 import os
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -28,16 +29,19 @@ def main(argv=None):
             ap.add_argument(name, type=float, default=f.default)
         else:
             ap.add_argument(name, default=f.default)
+    ap.add_argument("--pg-timeout", type=float, default=600.0,
+                    help="process-group timeout (s): a rank stuck in a collective fails the job instead of hanging")
     args = ap.parse_args(argv)
     cfg = TrainConfig(**{f.name: getattr(args, f.name) for f in dataclasses.fields(TrainConfig)})
+    pg_timeout = timedelta(seconds=args.pg_timeout)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not dist.is_initialized():
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if torch.cuda.is_available():
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=pg_timeout)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
     try:
         SimCLRTrainer(cfg).fit()
     finally:

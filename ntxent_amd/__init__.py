@@ -1,14 +1,18 @@
-"""Import alias for the framework package that lives in ``cuda-nt-xent-mpi-nccl-simclr_amd/``.
+"""Import name of the framework package that lives in ``cuda-nt-xent-mpi-nccl-simclr_amd/``.
 
-The on-disk package directory carries the project name (which is not a valid Python
-identifier); this shim points the ``ntxent_amd`` package's search path at it, so
-``import ntxent_amd.ops`` etc. resolve to the real modules there.
+The package directory carries the project name, which is not a valid Python identifier. This
+module loads that directory as the package ``ntxent_amd`` through importlib (spec with the real
+directory as its submodule search location) and puts the real package in ``sys.modules``, so
+``import ntxent_amd.ops`` etc. resolve to the modules there.
 """
+import importlib.util as _ilu
 import os as _os
+import sys as _sys
 
 _REAL = _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))),
                       "cuda-nt-xent-mpi-nccl-simclr_amd")
-__path__ = [_REAL]
-__file__ = _os.path.join(_REAL, "__init__.py")
-with open(__file__) as _f:
-    exec(compile(_f.read(), __file__, "exec"))
+_spec = _ilu.spec_from_file_location(__name__, _os.path.join(_REAL, "__init__.py"),
+                                     submodule_search_locations=[_REAL])
+_mod = _ilu.module_from_spec(_spec)
+_sys.modules[__name__] = _mod
+_spec.loader.exec_module(_mod)

@@ -147,12 +147,30 @@ def test_reference_api_forward_backward(ext):
     go = torch.tensor(1.0, device=h.device)
     gz, glog = ext.backward(h, lse, go, 0.07)
     gref = R.ntxent_backward_analytic(h.double().cpu(), 0.07)
-    assert (gz.double().cpu() - gref).abs().max() < 1e-4 * gref.abs().max() + 1e-9
+    # with the caller's fp32 LSE the positive coefficient a_i = 1 - P_ip inherits the LSE's
+    # rounding (~1e-6 absolute); these views are nearly saturated (P_ip -> 1, |grad| ~ 3e-6), so
+    # the stats path is held to that absolute level, the recomputing path to 1e-4 relative
+    assert (gz.double().cpu() - gref).abs().max() < 5e-3 * gref.abs().max() + 1e-9
     assert glog.shape == (64, 64)
     gz2, _ = torch.ops.ntxent_cuda.backward(h, torch.empty(64, 64, device=h.device), go, 0.07)
-    assert torch.allclose(gz, gz2, atol=1e-6)
+    assert (gz2.double().cpu() - gref).abs().max() < 1e-4 * gref.abs().max() + 1e-9
     assert torch.ops.ntxent_cuda.forward(h, 0.07).item() == pytest.approx(loss.item(), rel=1e-6)
     assert ext.check_tensor_core_support() is True
+
+
+@pytest.mark.parametrize("rows,dim,mp", [(600, 200, False), (2048, 512, True)])
+def test_raw_backward_with_stats_skips_forward(ext, rows, dim, mp):
+    """backward(z, lse_from_forward_with_stats, ...) runs ONE similarity GEMM (coefficients from
+    the given LSE) and matches the stateless path that recomputes the statistics."""
+    _, h = _inputs(rows, dim, torch.float32, seed=rows)
+    _, lse = ext.forward_with_stats(h, 0.1, use_mixed_precision=mp)
+    go = torch.tensor(0.5, device=h.device)
+    g1, _ = ext.backward(h, lse, go, 0.1, use_mixed_precision=mp)
+    g2, _ = ext.backward(h, torch.empty(0, device=h.device), go, 0.1, use_mixed_precision=mp)
+    scale = g2.abs().max().item()
+    assert (g1 - g2).abs().max().item() <= (1e-5 if not mp else 2e-3) * scale
+    gref = 0.5 * R.ntxent_backward_analytic(h.double().cpu(), 0.1)
+    assert (g1.double().cpu() - gref).abs().max().item() <= (2e-4 if not mp else 2e-2) * gref.abs().max().item()
 
 
 @pytest.mark.parametrize("B", [16, 32, 64, 128])
