@@ -785,13 +785,13 @@ int count_own_fwd_tiles(const Geometry& g) { return g.row_tiles * (g.row_tiles +
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   // Whole tiles in data-parallel rounds of G = num_cus blocks; only the remainder tiles
   // (ntiles % G) are split, into p K-pieces each, run by the first rem * p blocks after their
-  // DP rounds. A split tile costs its contributors a 256 KiB fp32 partial slab each and its
-  // last arriver p - 1 slab reads (~5 us per slab for one CU), while a piece saves nk/p
-  // K-steps (~2 us each), so p ~ sqrt(0.4 nk). The classic hybrid (one DP round fewer, that
-  // round plus the remainder split over every block) balanced K-steps exactly but split
-  // ~G + rem tiles: the forward GEMM at B = 4096 spent 30-74 us per block in slab traffic,
-  // the whole chip publishing at once. Splitting across all CUs when tiles < CUs
-  // (p = G / ntiles) made a small-batch dZ GEMM sum 32 slabs serially.
+  // DP rounds (the classic hybrid that also splits a whole DP round spent 30-74 us per block of
+  // the B = 4096 forward in slab traffic). p minimises, in K-step units,
+  //   nk / p + (p > 1 ? 10 + 4 (p - 1) : 0):
+  // a split costs ~10 K-steps once (slab publish, ticket, the last arriver's extra item) and ~4
+  // per partial slab the last arriver sums. Fitted on a same-box sweep of p = 1..8
+  // (profiles/r2/sk_split_sweep.log): p = 1 at nk <= 16 (d = 512 / 1024 forward; splitting cost
+  // 5-15 %), p = 3-4 at nk = 32 (the headline), p = 6 at nk = 128 (d = 8192, 36 tiles).
   GemmSchedule s;
   s.nk = nk;
   const int G0 = std::max(1, num_cus);
@@ -803,11 +803,15 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
     s.ipb = 0;
     return s;
   }
-  int p_opt = std::max(1, (int)std::lround(std::sqrt(0.4 * nk)));
+  int p = 1;
+  double best = 1e30;
+  for (int c = 1; c <= std::max(1, std::min(G0 / rem, nk)); ++c) {
+    const double cost = (double)nk / c + (c > 1 ? 10.0 + 4.0 * (c - 1) : 0.0);
+    if (cost < best - 1e-9) { best = cost; p = c; }
+  }
 #ifdef NTXENT_ABLATION_KERNELS
-  if (const char* e = std::getenv("NTXENT_SK_SPLIT")) p_opt = std::max(1, std::atoi(e));  // diagnostic builds only
+  if (const char* e = std::getenv("NTXENT_SK_SPLIT")) p = std::max(1, std::min({std::atoi(e), G0 / rem, nk}));  // diagnostic builds only
 #endif
-  const int p = std::max(1, std::min({p_opt, G0 / rem, nk}));
   s.grid = q > 0 ? G0 : rem * p;
   s.ipb = (nk + p - 1) / p;  // K-steps per stream-K block; ceil(rem * nk / ipb) <= rem * p blocks busy
   return s;

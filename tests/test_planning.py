@@ -66,7 +66,8 @@ def test_dz_tiles_cover_output(C):
 
 
 @pytest.mark.parametrize("ntiles,nk,cus", [(528, 32, 256), (256, 128, 256), (10, 4, 256), (1, 3, 256),
-                                           (300, 7, 256), (136, 16, 80), (1000, 2, 256)])
+                                           (300, 7, 256), (136, 16, 80), (1000, 2, 256), (36, 128, 256),
+                                           (528, 8, 256), (2080, 16, 256)])
 def test_stream_k_schedule(C, ntiles, nk, cus):
     s = C.schedule(ntiles, nk, cus)
     G = s["grid"]
@@ -88,9 +89,12 @@ def test_stream_k_schedule(C, ntiles, nk, cus):
             for t in range(lo // nk, (hi - 1) // nk + 1) if hi > lo else []:
                 pieces[t] = pieces.get(t, 0) + 1
         assert owned == total
-        # few contributors per split tile: the last arriver sums at most p_opt + 1 slabs
-        p_opt = max(1, round((0.4 * nk) ** 0.5))
+        # few contributors per split tile: the split p minimises nk/p + (p > 1: 10 + 4 (p - 1))
+        # (make_schedule's cost model); the last arriver sums at most p + 1 slabs
+        cands = range(1, max(1, min(cus // s["sk_tiles"], nk)) + 1)
+        p_opt = min(cands, key=lambda c: (nk / c + (10 + 4 * (c - 1) if c > 1 else 0), c))
         assert max(pieces.values()) <= p_opt + 1
+        assert s["ipb"] == -(-nk // p_opt)
     # balance: the busiest block does at most one DP round + ipb steps more than the mean
     mean = ntiles * nk / G
     worst = (s["dp_tiles"] // G) * nk + s["ipb"]
