@@ -62,3 +62,18 @@ def test_single_rank_cpu_json_contract():
         assert k in d
     assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+
+
+def test_scaling_driver_cpu():
+    """bench/scaling.py: runs bench.py per N and reports both efficiencies."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench" / "scaling.py"), "--ns", "1,2", "--device", "cpu",
+                        "--batch", "16", "--dim", "8", "--steps", "2", "--warmup", "1", "--dtype", "fp32",
+                        "--timeout", "120"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    doc = json.loads(r.stdout)
+    assert [c["n_gpus"] for c in doc["curve"]] == [1, 2]
+    c1, c2 = doc["curve"]
+    assert c1["samples_efficiency"] == pytest.approx(1.0) and c1["pair_efficiency"] == pytest.approx(1.0)
+    assert c2["pair_efficiency"] == pytest.approx(2 * c2["samples_efficiency"], rel=1e-3)  # JSON rounding
+    assert doc["runs"]["2"]["n_gpus"] == 2
