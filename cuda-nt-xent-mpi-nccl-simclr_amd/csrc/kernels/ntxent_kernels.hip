@@ -278,6 +278,86 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
   }
 }
 
+// Block-per-pair prologue for 2048 < d <= 2048 * NCH (d % 8 == 0): as prep_wave_kernel with 256
+// threads per pair, each thread keeping its NCH chunks of 8 features of both rows in registers,
+// so h is read once (the generic prep_kernel reads it twice: 1.5x the HBM traffic at d = 8192).
+template <typename Tin, typename Tc, bool Q8, int NCH>
+__global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
+                                                         float* __restrict__ inv, float* __restrict__ ypos,
+                                                         int R, int d, int dk, int ldk, float y_scale,
+                                                         unsigned char* __restrict__ zq8, int dk8, int ldk8) {
+  __shared__ float red[16];
+  const int t = threadIdx.x;
+  const int n = R >> 1, i = blockIdx.x, pi = i + n;
+  if (i >= n) {  // pad row R + (i - n) of zq (and zq8): zeros
+    zero_pad_row<Tc, Q8>(zq, zq8, R + (i - n), ldk, ldk8, t, 256);
+    return;
+  }
+  const Tin* hi = h + (long long)i * d;
+  const Tin* hp = h + (long long)pi * d;
+  Tc* zi = zq + (long long)i * ldk;
+  Tc* zp = zq + (long long)pi * ldk;
+  float a[NCH][8], b[NCH][8];
+  float ssi = 0.f, ssp = 0.f, mxi = 0.f, mxp = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 256 + t) * 8;
+    if (e < d) {
+      load8<Tin>(hi + e, a[c]);
+      load8<Tin>(hp + e, b[c]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[c][j] = 0.f; b[c][j] = 0.f; }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ssi += a[c][j] * a[c][j]; ssp += b[c][j] * b[c][j];
+      if constexpr (Q8) { mxi = fmaxf(mxi, fabsf(a[c][j])); mxp = fmaxf(mxp, fabsf(b[c][j])); }
+    }
+  }
+  ssi = block_sum(ssi, red);
+  ssp = block_sum(ssp, red + 8);
+  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
+  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  int ei = 0, ep = 0;
+  if constexpr (Q8) {
+    ei = fp8_row_exp(block_max(mxi, red) * ivi);
+    ep = fp8_row_exp(block_max(mxp, red + 8) * ivp);
+  }
+  const float sci = __int_as_float((ei + 127) << 23), scp = __int_as_float((ep + 127) << 23);
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int e = (c * 256 + t) * 8;
+    if (e < d) {
+      float qa[8], qb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a[c][j] *= ivi; b[c][j] *= ivp; }
+      store8<Tc>(zi + e, a[c], qa);
+      store8<Tc>(zp + e, b[c], qb);
+      if constexpr (Q8) {
+        *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa, sci);
+        *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb, scp);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dot += qa[j] * qb[j];
+    }
+  }
+  for (int e = d + t; e < dk; e += 256) { zi[e] = from_f32<Tc>(0.f); zp[e] = from_f32<Tc>(0.f); }
+  if constexpr (Q8) {
+    for (int e = d + t; e < dk8; e += 256) { zq8[(long long)i * ldk8 + e] = 0; zq8[(long long)pi * ldk8 + e] = 0; }
+    if (t == 0) {  // E8M0 scale byte right after the row's K range (see Geometry::ld_k8)
+      zq8[(long long)i * ldk8 + dk8] = (unsigned char)(127 - ei);
+      zq8[(long long)pi * ldk8 + dk8] = (unsigned char)(127 - ep);
+    }
+  }
+  dot = block_sum(dot, red);
+  if (t == 0) {
+    inv[i] = ivi; inv[pi] = ivp;
+    ypos[i] = dot * y_scale; ypos[pi] = dot * y_scale;
+  }
+}
+
 // 64x64 tile transpose with 16-byte global accesses on both sides (rows of Zq in, rows of
 // ZqT out); the LDS tile is padded by 16 B per row.
 template <typename T>
@@ -866,6 +946,24 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
         else by_q(std::integral_constant<int, 4>{});
         return;
       }
+      const int nbl = (g.dim % 8 == 0) ? (g.dim + 2047) / 2048 : 0;  // chunks per thread, 256 per pair
+      if (nbl >= 2 && nbl <= 8) {
+        auto go = [&](auto nc, auto q8) {
+          constexpr int NC = decltype(nc)::value;
+          constexpr bool Q = decltype(q8)::value;
+          hipLaunchKernelGGL((dev::prep_block_kernel<Tin, Tc, Q, NC>), dim3(g.rows / 2 + pad), dim3(256), 0, stream,
+                             static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim, g.dim_k,
+                             g.ld_k, ys, static_cast<unsigned char*>(zq8), g.dim_k8, g.ld_k8);
+        };
+        auto by_q = [&](auto nc) {
+          if (zq8) go(nc, std::true_type{});
+          else go(nc, std::false_type{});
+        };
+        if (nbl <= 2) by_q(std::integral_constant<int, 2>{});
+        else if (nbl <= 4) by_q(std::integral_constant<int, 4>{});
+        else by_q(std::integral_constant<int, 8>{});
+        return;
+      }
       if (zq8)
         hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, true>), dim3(g.rows / 2 + pad), dim3(256), 0, stream,
                            static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
@@ -965,7 +1063,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
   p.cpos = cpos;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(8 * ntiles), dim3(64), 0, stream, p);
+    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(16 * ntiles), dim3(64), 0, stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

@@ -913,26 +913,27 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if constexpr ((ABL & 64) != 0) tval(3, __builtin_amdgcn_s_memrealtime());
 }
 
-// Store-mode coefficient pass: one wave per 128x64 region (wm, wn) of a kept cosine tile
-// (canonical fragment order: 32 fragments of 512 B) -> C into the coefficient buffer. 17 KiB
-// of LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound).
+// Store-mode coefficient pass: one wave per 64x64 region (wm, wn, half) of a kept cosine tile
+// (canonical fragment order: 16 fragments of 512 B) -> C into the coefficient buffer. 9 KiB of
+// LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound), and 16
+// waves per tile keep a small problem's few tiles (36 at B = 1024/view) spread over the chip.
 template <typename T>
 __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
   const int lane = threadIdx.x;
   const int idx = xcd_remap(blockIdx.x, gridDim.x);
-  const int tidx = idx >> 3, w = idx & 7;
+  const int tidx = idx >> 4, w = (idx >> 1) & 7, half = idx & 1;
   const int wm = w >> 2, wn = w & 3;
   const int4 t = p.tiles[tidx];
   const T* st = reinterpret_cast<const T*>(p.sc) + (long long)tidx * kTileElems;
-  int rb[8], cb[4];
-  f32x4 acc[8][4];
+  int rb[4], cb[4];
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi) rb[mi] = 128 * wm + 16 * mi;
+  for (int mi = 0; mi < 4; ++mi) rb[mi] = 128 * wm + 64 * half + 16 * mi;
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) cb[ni] = 64 * wn + 16 * ni;
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
+  for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int np = 0; np < 2; ++np) {
       if constexpr (sizeof(T) == 2) {
@@ -948,14 +949,7 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
         }
       }
     }
-  // two 64-row halves through a 9 KiB staging tile: twice the resident waves of one 128-row
-  // pass (LDS-bound occupancy), more loads in flight on this HBM-bound pass
-  typedef f32x4 half_acc[4][4];
-  typedef int half_rb[4];
-  coef_epilogue<T, 1, 4>(*reinterpret_cast<half_acc*>(&acc[0]), *reinterpret_cast<const half_rb*>(&rb[0]), cb,
-                         128 * wm, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
-  coef_epilogue<T, 1, 4>(*reinterpret_cast<half_acc*>(&acc[4]), *reinterpret_cast<const half_rb*>(&rb[4]), cb,
-                         128 * wm + 64, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  coef_epilogue<T, 1, 4>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
 }
 
 }  // namespace dev

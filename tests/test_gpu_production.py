@@ -117,3 +117,14 @@ def test_grid_reserve_same_result(ext, reserve):
     assert old == 0
     assert abs(l1 - l0) <= 1e-6 * abs(l0)
     assert (g1.float() - g0.float()).abs().max().item() <= 1e-2 * g0.float().abs().max().item()
+
+
+@pytest.mark.parametrize("rows,dim,compute", [(512, 8192, "fp16"), (600, 3000, "bf16"), (256, 5000, "fp32")])
+def test_wide_rows_prep_block_path(ext, rows, dim, compute):
+    """d > 2048: the register-resident block-per-pair prologue (one read of h), BASELINE config 4
+    width and odd widths (3000 -> 2 chunks per thread, 5000 -> 4)."""
+    dt = torch.float32 if compute == "fp32" else torch.bfloat16
+    h = _views(rows, dim, seed=dim, dtype=dt)
+    lerr, gerr = _errors(h, 0.07, compute)
+    lt, gt = TOL[("fp32", "fp32")] if compute == "fp32" else TOL[("bf16", compute)]
+    assert lerr <= max(lt, 1e-6) and gerr <= gt, (lerr, gerr)
