@@ -211,8 +211,10 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 
 // dZ[Rpad][dim_n] = C * Z (fp32), C = the coefficient buffer, zqt_all = [W][dim_n][Rpad]
 // (all-gathered ZqT blocks); tiles from build_dz_tiles(g).
+// out_f16: write dZ as fp16 (the reduced-precision plans: half the bytes of the dZ store and of
+// the normalisation backward's read; |dZ| <= ~4, fp16 keeps 11 bits against the bf16/fp16 dh).
 void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
-               float* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream);
+               void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false);
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first
@@ -226,7 +228,8 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 
 // dh = grad_out/(2N tau) * inv * (g - z (z.g)), g = sum_ks slabs, z = h*inv (fp32).
 // xslabs (optional): nx more fp16 slabs [nx][Rpad][dim_n] added to the sum (received partner
-// contributions of the symmetric data-parallel mode).
+// contributions of the symmetric data-parallel mode, or the fp16 dZ of a reduced-precision plan
+// and nslabs = 0 fp32 slabs).
 void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h,
                      const float* inv, const float* grad_out, void* dh, const Geometry& g,
                      hipStream_t stream, const void* xslabs = nullptr, int nx = 0);

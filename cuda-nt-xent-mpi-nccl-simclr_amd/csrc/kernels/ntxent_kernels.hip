@@ -489,7 +489,11 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
     const int e = (c * 256 + threadIdx.x) * 8;
     if (e < d) {
       load8<Tin>(hi + e, z[c]);
-      f32x4 a = *reinterpret_cast<const f32x4*>(gi + e), b = *reinterpret_cast<const f32x4*>(gi + e + 4);
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+      if (nslabs > 0) {  // nslabs = 0: fp16 slabs only (xs)
+        a = *reinterpret_cast<const f32x4*>(gi + e);
+        b = *reinterpret_cast<const f32x4*>(gi + e + 4);
+      }
       for (int k = 1; k < nslabs; ++k) {
         a += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e);
         b += *reinterpret_cast<const f32x4*>(gi + k * slab_stride + e + 4);
@@ -1069,7 +1073,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 }
 
 void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
-               float* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream) {
+               void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16) {
   if (ntiles == 0) return;
   const long long cs = (long long)dtype_size(comp);
   dev::SimParams p = base_params(g);
@@ -1088,7 +1092,8 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.B.kblk_stride = (long long)g.dim_n * g.ld_t * cs;
   p.tiles = tiles;
   p.kbytes = (long long)g.world * g.rows_pad * cs;
-  p.out = slabs;
+  p.out = static_cast<float*>(slabs);
+  p.out_f16 = out_f16 ? 1 : 0;
   p.ldo = g.dim_n;
   p.slab_stride = (long long)g.rows_pad * g.dim_n;
   const int grid = apply_schedule(p, ntiles, ws, stream);

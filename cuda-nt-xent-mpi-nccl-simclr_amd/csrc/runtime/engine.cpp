@@ -191,12 +191,15 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.dz_gemm");
     fault_point("dz");
-    launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s);
+    launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32);
   }
   {
     NTXENT_TRACE("ntxent.norm_bwd");
     fault_point("norm_bwd");
-    launch_norm_bwd(cfg_.input, slabs_, 1, h_, inv_, grad_out ? grad_out : one_, dh, g_, s);
+    if (bwd_ != DType::F32)  // fp16 dZ slab (reduced-precision plans)
+      launch_norm_bwd(cfg_.input, nullptr, 0, h_, inv_, grad_out ? grad_out : one_, dh, g_, s, slabs_, 1);
+    else
+      launch_norm_bwd(cfg_.input, slabs_, 1, h_, inv_, grad_out ? grad_out : one_, dh, g_, s);
   }
 }
 

@@ -301,10 +301,12 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
   const at::DeviceGuard guard(sc.device());
-  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(sc, at::kFloat));
+  // reduced-precision plans keep dZ in fp16 (half the store and the normalisation backward's read)
+  const bool f16 = P.bwd() != DType::F32;
+  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(sc, f16 ? at::kHalf : at::kFloat));
   auto ws = gemm_ws(sc, P.n_dz, P);
   launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
-            P.n_dz, slabs.data_ptr<float>(), ws, P.g, cur_stream(sc));
+            P.n_dz, slabs.data_ptr(), ws, P.g, cur_stream(sc), f16);
   return slabs;
 }
 
@@ -314,8 +316,12 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
   const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
-  launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
-                  go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
+  if (slabs.scalar_type() == at::kHalf)  // one fp16 dZ slab (dz() of a reduced-precision plan)
+    launch_norm_bwd(to_dtype(h.scalar_type()), nullptr, 0, h.data_ptr(), inv.data_ptr<float>(), go.data_ptr<float>(),
+                    dh.data_ptr(), P.g, cur_stream(h), slabs.data_ptr(), 1);
+  else
+    launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
+                    go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
   return dh;
 }
 
