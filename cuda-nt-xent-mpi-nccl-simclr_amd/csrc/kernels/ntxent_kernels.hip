@@ -413,11 +413,23 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
   if (item < n) {  // uniform across the 8 lanes of an item
     const int i = item, j = item + n;
     float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
-    for (int t = q; t < Tc; t += kLseLanes) {
-      const float2 vi = part[(long long)t * Rpad + i];
-      const float2 vj = part[(long long)t * Rpad + j];
-      lse_merge(mi, si, vi.x, vi.y);
-      lse_merge(mj, sj, vj.x, vj.y);
+    // 4 column tiles per lane per round, all loads issued before the (branchy) merges: one
+    // memory round trip per 32 column tiles instead of one per tile
+    for (int t0 = q; t0 < Tc; t0 += 4 * kLseLanes) {
+      float2 vi[4], vj[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * kLseLanes;
+        const int tc = t < Tc ? t : t0;  // clamped (no conditional loads); duplicates are skipped below
+        vi[u] = part[(long long)tc * Rpad + i];
+        vj[u] = part[(long long)tc * Rpad + j];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (t0 + u * kLseLanes < Tc) {
+          lse_merge(mi, si, vi[u].x, vi[u].y);
+          lse_merge(mj, sj, vj[u].x, vj[u].y);
+        }
     }
 #pragma unroll
     for (int off = 1; off < kLseLanes; off <<= 1) {
