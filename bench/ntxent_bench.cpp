@@ -139,6 +139,8 @@ void* upload(std::vector<float>& host, DType in) {
   return d;
 }
 
+bool g_exp_backward = false;  // --exp: the coefficient-free backward (A/B against the coefficient pass)
+
 class Bench {
  public:
   Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed,
@@ -153,6 +155,7 @@ class Bench {
     c.keep_cos = keep_cos;
     c.small_path = small_path;
     c.small_splits = small_splits;
+    c.exp_backward = g_exp_backward;
     host_ = synthetic_views(c.rows, dim, seed);
     h_ = upload(host_, in);
     NTXENT_HIP_CHECK(hipMalloc(&dh_, host_.size() * dtype_size(in)));
@@ -343,12 +346,16 @@ int main(int argc, char** argv) {
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
     else if (a == "--no-small") o.small = false;
+    else if (a == "--exp") g_exp_backward = true;
+    else if (a == "--no-exp") g_exp_backward = false;
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
                   "                    [--recompute] [--no-small] [--gpus N] [--json out.json]\n"
-                  "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n");
+                  "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n"
+                  "  --exp / --no-exp: coefficient-free backward (exponential store, C formed in the dZ GEMM) or\n"
+                  "                    the coefficient pass + dZ GEMM (default)\n");
       return 0;
     }
   }

@@ -480,14 +480,25 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
 // Vectorised normalisation backward: one 256-thread block per row; each thread owns NCH
 // chunks of 8 contiguous features, kept in registers between the dot pass and the output.
 // xs: nx extra fp16 slabs (received partner contributions, symmetric data-parallel mode) added
-// to the fp32 sum.
+// to the fp32 sum. zdt != 0 (exponential backward, whose dZ GEMM leaves the positive pair out):
+// g += cpos[i] * zq[p(i)], zq rows zld elements apart in fp16 (zdt 1) or bf16 (zdt 2).
+struct PosArgs {
+  const void* zq;
+  const float* cpos;
+  int zld, zdt, n_half;
+};
+__device__ __forceinline__ void pos_load8(const PosArgs& pa, int i, int e, float (&v)[8]) {
+  const long long ip = i < pa.n_half ? i + pa.n_half : i - pa.n_half;
+  if (pa.zdt == 1) load8<_Float16>(static_cast<const _Float16*>(pa.zq) + ip * pa.zld + e, v);
+  else load8<__bf16>(static_cast<const __bf16*>(pa.zq) + ip * pa.zld + e, v);
+}
 template <typename Tin, int NCH>
 __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int nslabs,
                                                            long long slab_stride, long long ldo,
                                                            const Tin* __restrict__ h, const float* __restrict__ inv,
                                                            const float* __restrict__ grad_out, float alpha_base,
                                                            Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
-                                                           int nx) {
+                                                           int nx, const PosArgs pa) {
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -517,6 +528,13 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
       }
       g[c][0] = a[0]; g[c][1] = a[1]; g[c][2] = a[2]; g[c][3] = a[3];
       g[c][4] = b[0]; g[c][5] = b[1]; g[c][6] = b[2]; g[c][7] = b[3];
+      if (pa.zdt != 0) {
+        float zp[8];
+        pos_load8(pa, i, e, zp);
+        const float cp = pa.cpos[i];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[c][j] += cp * zp[j];
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) { z[c][j] *= iv; dot += z[c][j] * g[c][j]; }
     }
@@ -542,8 +560,15 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
                                                        const Tin* __restrict__ h, const float* __restrict__ inv,
                                                        const float* __restrict__ grad_out, float alpha_base,
                                                        Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
-                                                       int nx) {
+                                                       int nx, const PosArgs pa) {
   const _Float16* xi = xs + (long long)blockIdx.x * ldo;
+  const long long ip = blockIdx.x < pa.n_half ? blockIdx.x + pa.n_half : (long long)blockIdx.x - pa.n_half;
+  const float cp = pa.zdt != 0 ? pa.cpos[blockIdx.x] : 0.f;
+  auto zpos = [&](int e) -> float {
+    if (pa.zdt == 0) return 0.f;
+    return pa.zdt == 1 ? (float)static_cast<const _Float16*>(pa.zq)[ip * pa.zld + e]
+                       : (float)static_cast<const __bf16*>(pa.zq)[ip * pa.zld + e];
+  };
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -555,6 +580,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
     float g = 0.f;
     for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
+    g += cp * zpos(e);
     dot += to_f32<Tin>(hi[e]) * iv * g;
   }
   dot = block_sum(dot, red);
@@ -563,6 +589,7 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
     float g = 0.f;
     for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
+    g += cp * zpos(e);
     const float z = to_f32<Tin>(hi[e]) * iv;
     di[e] = from_f32<Tin>(alpha * iv * (g - z * dot));
   }
@@ -619,11 +646,20 @@ int gemm_ablation() {
 template <typename Tc, int MODE>
 void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
 #ifdef NTXENT_ABLATION_KERNELS
+  if constexpr (MODE == dev::kModeDzE && std::is_same<Tc, _Float16>::value) switch (gemm_ablation()) {
+    // coefficient-free dZ: 1 no DMA, 2 no A reads, 4 no MFMA, 128 no transform, 64 timeline
+#define NTXENT_ABL_E(A) \
+    case A: hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); return;
+    NTXENT_ABL_E(1) NTXENT_ABL_E(2) NTXENT_ABL_E(4) NTXENT_ABL_E(128) NTXENT_ABL_E(129) NTXENT_ABL_E(130)
+    NTXENT_ABL_E(6) NTXENT_ABL_E(134) NTXENT_ABL_E(256) NTXENT_ABL_E(512) NTXENT_ABL_E(258) NTXENT_ABL_E(514) NTXENT_ABL_E(1152) NTXENT_ABL_E(2176)
+#undef NTXENT_ABL_E
+    default: break;
+  }
   if constexpr (std::is_same<Tc, _Float16>::value || std::is_same<Tc, dev::fp8e4m3>::value) switch (gemm_ablation()) {
     // fp8: only the timeline build (64) is instantiated
 #define NTXENT_ABL_CASE(A) \
     case A:                                                                                                  \
-      if constexpr (std::is_same<Tc, _Float16>::value || (A == 1 && std::is_same<Tc, dev::fp8e4m3>::value)) { \
+      if constexpr ((std::is_same<Tc, _Float16>::value && MODE != dev::kModeDzE) || (A == 1 && std::is_same<Tc, dev::fp8e4m3>::value)) { \
         hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); \
         return;                                                                                              \
       }                                                                                                      \
@@ -1004,7 +1040,7 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream, const BlockView& bv, float2* part_x) {
+                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp) {
   if (ntiles == 0) return;
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
@@ -1019,6 +1055,11 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.sc = static_cast<char*>(sc);
   p.b_tile0 = bv.b_tile0;
   p.part_x = part_x;
+  if (store_exp) {
+    NTXENT_CHECK(exp_backward_eligible(g, comp) && sc != nullptr && bv.b_tile0 == 0 && part_x == nullptr,
+                 "fwd_stats: exponential store needs an exp-backward plan (see exp_backward_eligible)");
+    p.store_exp = 1;
+  }
   const int grid = apply_schedule(p, ntiles, ws, stream);
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
@@ -1116,6 +1157,52 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
+bool exp_backward_eligible(const Geometry& g, DType comp) {
+  const float M = g.inv_temp * dev::kLog2e;
+  return comp != DType::F32 && 2.0f * M < 120.0f && (long long)g.col_tiles * kTile <= dev::kExpMaxRows;
+}
+
+size_t exp_store_elems(const Geometry& g) {
+  const long long rt = g.row_tiles;
+  return (size_t)((rt * (rt + 1) / 2 + rt * (g.col_tiles - rt)) * kTileElems);
+}
+
+int exp_coef_shift(const Geometry& g) {
+  int s = 0;
+  while ((2LL << s) <= g.global_rows) ++s;  // floor(log2(2N))
+  return std::max(0, std::min(14, s - 3));
+}
+
+void launch_dz_exp(DType comp, const void* ebuf, const void* zqt_all, const float* lse2_all, const int4* tiles,
+                   int ntiles, void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
+                   bool out_f16) {
+  if (ntiles == 0) return;
+  const DType bc = backward_dtype(comp);
+  NTXENT_CHECK(exp_backward_eligible(g, comp), "dz_exp: plan not eligible for the exponential backward");
+  const long long cs = 2;
+  dev::SimParams p = base_params(g);
+  p.sc = const_cast<char*>(static_cast<const char*>(ebuf));
+  p.lse2 = lse2_all;
+  const int sh = exp_coef_shift(g);
+  p.a_shift = p.y_scale + (float)sh;
+  p.out_scale = std::ldexp(1.0f, -sh);
+  p.B.base = static_cast<const char*>(zqt_all);
+  p.B.ld = (long long)g.ld_t * cs;
+  p.B.row_tile_stride = (long long)kTile * g.ld_t * cs;
+  p.B.kblk = (long long)g.rows_pad * cs;
+  p.B.kblk_stride = (long long)g.dim_n * g.ld_t * cs;
+  p.tiles = tiles;
+  p.kbytes = (long long)g.world * g.rows_pad * cs;
+  p.out = static_cast<float*>(dz);
+  p.out_f16 = out_f16 ? 1 : 0;
+  p.ldo = g.dim_n;
+  p.slab_stride = (long long)g.rows_pad * g.dim_n;
+  const int grid = apply_schedule(p, ntiles, ws, stream);
+  if (bc == DType::BF16) launch_sim_gemm<__bf16, dev::kModeDzE>(grid, p, stream);
+  else launch_sim_gemm<_Float16, dev::kModeDzE>(grid, p, stream);
+  NTXENT_HIP_CHECK(hipGetLastError());
+}
+
 void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
                     long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, void* out, bool accum,
                     const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16) {
@@ -1153,8 +1240,14 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 
 void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h, const float* inv,
                      const float* grad_out, void* dh, const Geometry& g, hipStream_t stream,
-                     const void* xslabs, int nx) {
+                     const void* xslabs, int nx, const PosTerm& pos) {
   const _Float16* xs = static_cast<const _Float16*>(xslabs);
+  dev::PosArgs pa{pos.zq, pos.cpos, pos.ld, 0, g.rows / 2};
+  if (pos.zq != nullptr) {
+    NTXENT_CHECK(pos.cpos != nullptr && (pos.zdt == DType::F16 || pos.zdt == DType::BF16) && pos.ld >= g.dim,
+                 "norm_bwd: bad positive-pair term");
+    pa.zdt = pos.zdt == DType::F16 ? 1 : 2;
+  }
   if (xs == nullptr) nx = 0;
   const float alpha_base = (float)(1.0 / ((double)g.global_rows * g.temperature));
   const long long ss = (long long)g.rows_pad * g.dim_n, ldo = g.dim_n;
@@ -1166,16 +1259,16 @@ void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h, co
     Tin* dp = static_cast<Tin*>(dh);
     if (vec && nch == 1)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
     else if (vec && nch == 2)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
     else if (vec)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
     else
       hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss, ldo,
-                         hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
+                         hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

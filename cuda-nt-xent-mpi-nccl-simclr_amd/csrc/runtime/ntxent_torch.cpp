@@ -65,6 +65,8 @@ struct Plan {
   int n_dz = 0;
   int num_cus = 256;
   bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
+  // coefficient-free backward: the single-process flow keeps exponentials (exp_backward_eligible)
+  bool exp_bwd = false;
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
@@ -113,6 +115,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
   p->small = small_path_eligible(p->g, comp);
+  p->exp_bwd = exp_backward_eligible(p->g, comp);
   cache.emplace(key, p);
   return p;
 }
@@ -125,6 +128,12 @@ static void check_input(const at::Tensor& h, const char* name) {
   NTXENT_CHECK(h.is_cuda(), std::string(name) + " must be a GPU (HIP) tensor");
   NTXENT_CHECK(h.is_contiguous(), std::string(name) + " must be contiguous");
 }
+
+// Coefficient-free backward switch (off by default while its dZ GEMM is slower than the
+// coefficient pass + dZ GEMM it replaces; see tests/test_gpu_expbwd.py, profiles/r2/expbwd).
+static std::atomic<bool> g_exp_backward{false};
+void set_exp_backward(bool on) { g_exp_backward = on; }
+bool exp_backward_enabled() { return g_exp_backward.load(); }
 
 static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
   return at::TensorOptions().dtype(t).device(like.device());
@@ -215,7 +224,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
 }
 
 std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P,
-                                  bool keep_cos) {
+                                  bool keep_cos, bool store_exp = false) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.op_ld(),
@@ -223,12 +232,15 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  // the exponential store is returned 3-D [slots, 256, 256] (cosines: flat), which is how the
+  // backward tells the two apart
+  if (store_exp) sc = at::empty({(long)(exp_store_elems(P.g) / kTileElems), kTile, kTile}, opts(zq_local, at::kBFloat16));
+  else if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
-                   reinterpret_cast<float2*>(part.data_ptr<float>()), keep_cos ? sc.data_ptr() : nullptr,
-                   ws, P.g, cur_stream(zq_local));
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), sc.defined() ? sc.data_ptr() : nullptr,
+                   ws, P.g, cur_stream(zq_local), BlockView{}, nullptr, store_exp);
   return {part, sc};
 }
 
@@ -310,15 +322,46 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   return slabs;
 }
 
+// Exponential store (fwd_stats store_exp) -> dZ without the positive pair (fp16 slab), see
+// launch_dz_exp; norm_bwd(..., zq, cpos) adds it back.
+at::Tensor dz_exp(const at::Tensor& ebuf, const at::Tensor& zqt_all, const at::Tensor& lse2_all, const Plan& P) {
+  check_input(ebuf, "ebuf");
+  check_input(zqt_all, "zqt_all");
+  NTXENT_CHECK(P.exp_bwd, "dz_exp: plan is not eligible for the exponential backward");
+  NTXENT_CHECK(ebuf.numel() == (long)exp_store_elems(P.g) && ebuf.scalar_type() == at::kBFloat16,
+               "ebuf must be the bf16 exponential store of the plan");
+  NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
+  NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad, "lse2_all must be [world*rows_pad]");
+  const at::DeviceGuard guard(ebuf.device());
+  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(ebuf, at::kHalf));
+  auto ws = gemm_ws(ebuf, P.n_dz, P);
+  launch_dz_exp(P.comp, ebuf.data_ptr(), zqt_all.data_ptr(), lse2_all.data_ptr<float>(),
+                reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws, P.g,
+                cur_stream(ebuf), /*out_f16=*/true);
+  return slabs;
+}
+
 at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
-                    const Plan& P) {
+                    const Plan& P, const c10::optional<at::Tensor>& zq_pos_in = c10::nullopt,
+                    const c10::optional<at::Tensor>& cpos_in = c10::nullopt) {
+  const at::Tensor zq_pos = zq_pos_in.has_value() ? *zq_pos_in : at::Tensor();
+  const at::Tensor cpos = cpos_in.has_value() ? *cpos_in : at::Tensor();
   check_input(h, "h");
   const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
+  PosTerm pos;
+  if (zq_pos.defined()) {  // exponential backward: the positive pair's term
+    NTXENT_CHECK(cpos.defined() && cpos.numel() >= P.g.rows && zq_pos.numel() >= (long)P.g.rows * P.g.ld_k,
+                 "norm_bwd: positive term needs zq [rows_pad, ld_k] and cpos");
+    pos.zq = zq_pos.data_ptr();
+    pos.zdt = to_dtype(zq_pos.scalar_type());
+    pos.ld = P.g.ld_k;
+    pos.cpos = cpos.data_ptr<float>();
+  }
   if (slabs.scalar_type() == at::kHalf)  // one fp16 dZ slab (dz() of a reduced-precision plan)
     launch_norm_bwd(to_dtype(h.scalar_type()), nullptr, 0, h.data_ptr(), inv.data_ptr<float>(), go.data_ptr<float>(),
-                    dh.data_ptr(), P.g, cur_stream(h), slabs.data_ptr(), 1);
+                    dh.data_ptr(), P.g, cur_stream(h), slabs.data_ptr(), 1, pos);
   else
     launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
                     go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
@@ -611,7 +654,10 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
-  auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
+  // plans eligible for the coefficient-free backward keep exponentials instead of cosines
+  const bool keep = keep_cos || f8;
+  const bool ex = P->exp_bwd && g_exp_backward.load();
+  auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true, ex) : fwd_stats(pr[0], pr[0], *P, keep, keep && ex);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
@@ -637,6 +683,10 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     return dh;
   }
   at::Tensor cb;
+  if (sc_in.has_value() && sc_in->defined() && sc_in->dim() == 3) {  // kept exponentials: no coefficient pass
+    auto slabs = dz_exp(*sc_in, zqt, lse2, *P);
+    return norm_bwd(slabs, h, inv, grad_out, *P, zq, cpos);
+  }
   if (sc_in.has_value() && sc_in->defined()) {
     cb = coef(*sc_in, lse2, cpos, *P);
   } else {
@@ -773,6 +823,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("small", &Plan::small)
+      .def_readonly("exp_bwd", &Plan::exp_bwd)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
   m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
@@ -785,12 +836,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"));
-  m.def("fwd_stats", &fwd_stats);
+  m.def("fwd_stats", &fwd_stats, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"),
+        py::arg("store_exp") = false);
   m.def("lse", &lse);
   m.def("coef", &coef);
   m.def("coef_gemm", &coef_gemm);
   m.def("dz", &dz);
-  m.def("norm_bwd", &norm_bwd);
+  m.def("set_exp_backward", &set_exp_backward, py::arg("on"));
+  m.def("exp_backward_enabled", &exp_backward_enabled);
+  m.def("dz_exp", &dz_exp, py::arg("ebuf"), py::arg("zqt_all"), py::arg("lse2_all"), py::arg("plan"));
+  m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"),
+        py::arg("zq_pos") = py::none(), py::arg("cpos") = py::none());
   m.def("fwd_stats_tiles", &fwd_stats_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
         py::arg("tiles"), py::arg("plan"), py::arg("part"));
   m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
