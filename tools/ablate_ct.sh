@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 if [ "$1" = "build" ]; then
   INC=$ROOT/cuda-nt-xent-mpi-nccl-simclr_amd/csrc/include
   mkdir -p $ROOT/build/abl
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -fPIC -O3 -DNTXENT_ABLATION_KERNELS -I$INC \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -std=c++17 -fPIC -O3 ${ABL_EXTRA_FLAGS} -DNTXENT_ABLATION_KERNELS -I$INC \
     -c $ROOT/cuda-nt-xent-mpi-nccl-simclr_amd/csrc/kernels/ntxent_kernels.hip -o $ROOT/build/abl/k.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 $ROOT/build/ntxent_bench.o $ROOT/build/abl/k.o $ROOT/build/small_kernels.o $ROOT/build/engine.o \
     $ROOT/build/rccl_comm.o $ROOT/build/trace.o -o $ROOT/build/bin/ntxent_bench_abl -L/opt/rocm/lib -lrccl -ldl \
