@@ -113,9 +113,11 @@ struct SymJob {
 std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs, int nchunks = 1);
 
 // Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
-// first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered.
+// first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered; its
+// last own_diag_tail(g) entries are the diagonal tiles (kTileDiag).
 std::vector<int4> build_fwd_tiles(const Geometry& g);
 int count_own_fwd_tiles(const Geometry& g);
+int own_diag_tail(const Geometry& g);
 // dZ tiles (ti, tn, 0, 0): the persistent stream-K schedule balances K itself (no split-K).
 std::vector<int4> build_dz_tiles(const Geometry& g);
 
@@ -179,10 +181,19 @@ struct BlockView {
 // store_exp (exp_backward_eligible plans, all-gather layout): keep E = 2^(y - M) (bf16) in
 // `sc` instead of the cosines, exp_store_elems(g) elements in exp_slot order (own-block upper
 // triangle, then the remote tiles), masked elements (self, positive, padding) exactly 0.
+// diag_tail: the last `diag_tail` entries of `tiles` are kTileDiag tiles (own_diag_tail(g) for
+// a launch that ends with the own block, else 0). When the persistent GEMM's tile count leaves a
+// remainder of at most that many tiles after its whole rounds, the remainder runs as 16-row
+// strips in a second, short launch (diag_strip_kernel) instead of a third round or a stream-K
+// split (528 forward tiles at B = 4096/view: 2 rounds + strips instead of ~2.9 rounds).
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                      const BlockView& bv = BlockView{}, float2* part_x = nullptr, bool store_exp = false);
+                      const BlockView& bv = BlockView{}, float2* part_x = nullptr, bool store_exp = false,
+                      int diag_tail = 0);
+// Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
+void set_diag_strips(bool on);
+bool diag_strips_enabled();
 
 // ---- coefficient-free backward ---------------------------------------------------------------
 // Plans whose forward can keep exponentials for it: reduced precision, fixed-shift epilogue

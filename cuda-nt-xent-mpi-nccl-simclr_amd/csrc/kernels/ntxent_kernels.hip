@@ -16,6 +16,7 @@
 #include "device_common.h"
 #include "sim_gemm.h"
 
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -865,33 +866,40 @@ static void zorder(std::vector<int4>& t, size_t first, size_t last) {
   });
 }
 
+// Own-block upper triangle: the off-diagonal tiles in Z-order, then the row_tiles diagonal
+// tiles in order (own_diag_tail(g) of them end the list).
+static std::vector<int4> own_block_tiles(const Geometry& g) {
+  std::vector<int4> tiles;
+  const int own = g.rank * g.row_tiles;
+  for (int ti = 0; ti < g.row_tiles; ++ti)
+    for (int local = ti + 1; local < g.row_tiles; ++local) tiles.push_back(make_int4(ti, own + local, kTileSymOff, 0));
+  zorder(tiles, 0, tiles.size());
+  for (int ti = 0; ti < g.row_tiles; ++ti) tiles.push_back(make_int4(ti, own + ti, kTileDiag, 0));
+  return tiles;
+}
+
+int own_diag_tail(const Geometry& g) { return g.row_tiles; }
+
 std::vector<int4> build_fwd_tiles(const Geometry& g) {
   // Own-rank block first (upper triangle: S is symmetric), then the remote column blocks.
   // Each part in Z-order: the blocks of one XCD (consecutive logical ids after xcd_remap) take
   // consecutive tiles, and a Z-order run of 32 tiles touches ~0.4 distinct row panels per tile
   // (A and B panels of the own block are both rows of Zq) versus ~0.7-1.0 for panel-major
   // order, which is what the forward GEMM's L2 hit rate depends on (measured 48% before).
-  std::vector<int4> tiles;
-  const int own = g.rank * g.row_tiles;
-  for (int ti = 0; ti < g.row_tiles; ++ti)
-    for (int local = ti; local < g.row_tiles; ++local)
-      tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
+  // The own block's diagonal tiles come last in it (own_block_tiles): a launch of the own block
+  // leaves its whole-round remainder on them, which the strip kernel finishes (launch_fwd_stats).
+  std::vector<int4> tiles = own_block_tiles(g);
   const size_t n_own = tiles.size();
+  const int own = g.rank * g.row_tiles;
   for (int ti = 0; ti < g.row_tiles; ++ti)
     for (int tj = 0; tj < g.col_tiles; ++tj)
       if (tj < own || tj >= own + g.row_tiles) tiles.push_back(make_int4(ti, tj, kTilePlain, 0));
-  zorder(tiles, 0, n_own);
   zorder(tiles, n_own, tiles.size());
   return tiles;
 }
 
 std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs, int nchunks) {
-  std::vector<int4> tiles;
-  const int own = g.rank * g.row_tiles;
-  for (int ti = 0; ti < g.row_tiles; ++ti)
-    for (int local = ti; local < g.row_tiles; ++local)
-      tiles.push_back(make_int4(ti, own + local, local == ti ? kTileDiag : kTileSymOff, 0));
-  zorder(tiles, 0, tiles.size());
+  std::vector<int4> tiles = own_block_tiles(g);
   for (const SymJob& j : jobs) {
     NTXENT_CHECK(j.q >= 0 && j.q < g.world && j.q != g.rank, "sym job: bad partner");
     NTXENT_CHECK(0 <= j.m0 && j.m0 <= j.m1 && j.m1 <= g.row_tiles && 0 <= j.k0 && j.k0 <= j.k1 &&
@@ -1038,10 +1046,15 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
+static std::atomic<bool> g_diag_strips{true};
+void set_diag_strips(bool on) { g_diag_strips = on; }
+bool diag_strips_enabled() { return g_diag_strips.load(); }
+
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp) {
+                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp, int diag_tail) {
   if (ntiles == 0) return;
+  NTXENT_CHECK(diag_tail >= 0 && diag_tail <= ntiles, "fwd_stats: bad diagonal tail");
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
   const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
@@ -1060,10 +1073,37 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
                  "fwd_stats: exponential store needs an exp-backward plan (see exp_backward_eligible)");
     p.store_exp = 1;
   }
-  const int grid = apply_schedule(p, ntiles, ws, stream);
+  // Whole rounds on the persistent GEMM; a remainder that fits in the diagonal tail runs as
+  // strips (diag_strip_kernel) after it instead of as a third round / stream-K split. fp8 and
+  // exponential-store launches keep the stream-K schedule.
+  int nstrip = 0;
+  if (diag_tail > 0 && comp != DType::FP8 && !store_exp && diag_strips_enabled()) {
+    const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+    const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
+    if (q >= 1 && rem > 0 && rem <= diag_tail) nstrip = rem;
+  }
+  const int nmain = ntiles - nstrip;
+  const int grid = apply_schedule(p, nmain, ws, stream);
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
+    if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
+      if (nstrip > 0) {
+        NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diag strips: row-major operands only");
+        dev::SimParams q = p;
+        q.tiles = tiles + nmain;
+        if (q.sc) q.sc += (size_t)nmain * kTileElems * sizeof(typename dev::StoreT<Tc>::type);
+        const dim3 sg(nstrip * 16);
+        const bool one_wave = nstrip * 16 <= ws.num_cus;  // 3-stage ring, else 2 blocks per CU
+        if (p.fixed_shift) {
+          if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 3>), sg, dim3(256), 0, stream, q);
+          else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q);
+        } else {
+          if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 0, 3>), sg, dim3(256), 0, stream, q);
+          else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 0, 2>), sg, dim3(256), 0, stream, q);
+        }
+      }
+    }
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

@@ -1257,5 +1257,163 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   coef_epilogue<T, 1, 4>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
 }
 
+// ------------------------------------------------------------------------------------
+// Diagonal-tile strips: the remainder of the forward's whole rounds (launch_fwd_stats).
+// A diagonal tile S_tt is symmetric, so its row partials are all the epilogue owes and its
+// 16-row strips are independent: one 4-wave block per strip (16 blocks per tile), wave w owns
+// columns [64w, 64w + 64) (4 fragments of 16x16) and runs on its own: it LDS-DMAs the strip's
+// 16 A rows and its 64 B rows (80 rows x 128 B per K-step, whole lines, 8 rows per instruction)
+// into its private 3-stage ring and reads the fragments back with conflict-free ds_read_b128
+// (chunk ^ ((row >> 1) & 7) swizzle on the source address, as the GEMM). Only the wave's own
+// counted vmcnt orders its reads behind its DMA, so the K loop has no barrier. (Fragment-shaped
+// loads straight to registers put 16 rows in every instruction's 16 lanes and ran 4x slower.)
+// Row partials are merged over the 4 waves in LDS; masks, the fixed-shift / per-row-max
+// partials and the kept-cosine layout are the GEMM epilogue's.
+// ------------------------------------------------------------------------------------
+// NST = ring depth: 3 stages (120 KiB, one block per CU) when the strips fit in one wave of
+// blocks, 2 (80 KiB, two blocks per CU) when there are more strips than CUs. The row-partial
+// merge reuses wave 0's ring after every wave has left its K loop.
+constexpr int kStripRows = 80;                                   // 16 A rows + 64 B rows per wave
+constexpr int kStripStage = kStripRows * kKStepBytes;            // 10 KiB
+
+template <typename T, int FX, int NST>
+__global__ __launch_bounds__(256) void diag_strip_kernel(const SimParams p) {
+  constexpr int kStripStages = NST;
+  constexpr int kStripWaveLds = kStripStages * kStripStage;
+  constexpr int kStripLds = 4 * kStripWaveLds;
+  using MM = Mfma<T>;
+  typedef typename MM::frag frag;
+  typedef typename StoreT<T>::type TS;
+  typedef __attribute__((address_space(3))) const frag lds_frag;
+  // one LDS array (a second __shared__ object makes hipcc drain the LDS-DMA before ds_reads)
+  __shared__ __attribute__((aligned(16))) char smem[kStripLds];
+  lds_char* lds = (lds_char*)smem;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 strips share one XCD's L2
+  const int tile = idx >> 4, strip = idx & 15;
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y;
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  // DMA piece j (j < 10) = ring rows [8j, 8j + 8): rows 0-15 the strip's A rows, 16-79 this
+  // wave's B rows; lane -> row 8j + (lane >> 3), 16-byte chunk (lane & 7) ^ ((row >> 1) & 7)
+  const char* src[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int row = 8 * j + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    src[j] = row < 16 ? p.A.base + (long long)mt * p.A.row_tile_stride + (long long)(16 * strip + row) * p.A.ld + 16 * chunk
+                      : p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride +
+                            (long long)(64 * w + row - 16) * p.B.ld + 16 * chunk;
+  }
+  lds_char* ring = lds + w * kStripWaveLds;
+  auto stage = [&](int s, int buf) {
+    const long long o = (long long)s * kKStepBytes;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + o), (lds_void*)(ring + buf * kStripStage + j * 8 * kKStepBytes),
+                                       16, 0, 0);
+  };
+  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
+  f32x4 acc[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue: steps 0 .. NST-1 (clamped: trailing prefetches re-read the last step)
+#pragma unroll
+  for (int i = 0; i < kStripStages; ++i) stage(i < nk ? i : nk - 1, i);
+  int buf = 0;
+  for (int s = 0; s < nk; ++s) {
+    // step s landed (the NST - 1 younger steps' 10 pieces each still in flight)
+    if constexpr (kStripStages == 3) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    const lds_char* st = ring + buf * kStripStage;
+    frag af[2], bf[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int pch = ((4 * c + cq) ^ sw) << 4;
+      af[c] = *(lds_frag*)(st + r16 * kKStepBytes + pch);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) bf[c][f] = *(lds_frag*)(st + (16 + 16 * f + r16) * kKStepBytes + pch);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done: the stage may be refilled
+    __builtin_amdgcn_sched_barrier(0);
+    const int nx = s + kStripStages;
+    stage(nx < nk ? nx : nk - 1, buf);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] = MM::mma(af[c], bf[c][f], acc[f]);
+    buf = buf == kStripStages - 1 ? 0 : buf + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
+  // lane holds S[row 16 strip + 4 (lane >> 4) + r][col 64 w + 16 f + (lane & 15)] (tile-local)
+  const int rb0 = 16 * strip;
+  if (p.sc) {  // kept cosines, canonical fragment order (sc_unit), before the masks
+    TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
+    const float cs = p.cos_scale;
+    if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+      for (int np = 0; np < 2; ++np) {
+        union { TS h[8]; u32x4 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pk.h[r] = from_f32<TS>(acc[2 * np][r] * cs);
+          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r] * cs);
+        }
+        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * w + 32 * np, lane) * 8) = pk.u;
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * w + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f] * cs;
+    }
+  }
+  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
+  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+  const float sc_ = p.acc_scale, M = p.y_scale;
+  float2 part[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tr = rb0 + 4 * (lane >> 4) + r, gi = r0 + tr;
+    float y[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int tc = 64 * w + 16 * f + (lane & 15), d = tc - tr;
+      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
+                        ((d == D2) & (gi >= p.n_half));
+      y[f] = drop ? kNegInf : acc[f][r] * sc_;
+    }
+    if constexpr (FX != 0) {
+      float s = (fast_exp2(y[0] - M) + fast_exp2(y[1] - M)) + (fast_exp2(y[2] - M) + fast_exp2(y[3] - M));
+      s = row16_sum(s);
+      part[r] = make_float2(s > 0.f ? M : kNegInf, s);
+    } else {
+      float m = fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3]));
+      m = row16_max(m);
+      const float ms = (m == kNegInf) ? 0.f : m;
+      float s = (fast_exp2(y[0] - ms) + fast_exp2(y[1] - ms)) + (fast_exp2(y[2] - ms) + fast_exp2(y[3] - ms));
+      s = row16_sum(s);
+      part[r] = make_float2(m, s);
+    }
+  }
+  typedef __attribute__((address_space(3))) float lds_fl;
+  lds_fl* red = (lds_fl*)lds;  // [4 waves][16 rows] x (max, sum), over wave 0's drained ring
+  __syncthreads();
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      red[2 * (w * 16 + 4 * (lane >> 4) + r)] = part[r].x;
+      red[2 * (w * 16 + 4 * (lane >> 4) + r) + 1] = part[r].y;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int i = threadIdx.x;
+    float m = red[2 * i], s = red[2 * i + 1];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) lse_merge(m, s, red[2 * (q * 16 + i)], red[2 * (q * 16 + i) + 1]);
+    p.part[(long long)nt * p.Rpad + r0 + rb0 + i] = make_float2(m, s);
+  }
+}
+
 }  // namespace dev
 }  // namespace ntxent

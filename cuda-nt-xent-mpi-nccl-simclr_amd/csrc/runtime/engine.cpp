@@ -145,7 +145,7 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s, BlockView{},
-                     nullptr, exp_);
+                     nullptr, exp_, own_diag_tail(g_));
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");

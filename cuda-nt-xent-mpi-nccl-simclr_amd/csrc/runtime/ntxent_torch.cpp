@@ -240,7 +240,8 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), sc.defined() ? sc.data_ptr() : nullptr,
-                   ws, P.g, cur_stream(zq_local), BlockView{}, nullptr, store_exp);
+                   ws, P.g, cur_stream(zq_local), BlockView{}, nullptr, store_exp,
+                   P.n_fwd == P.n_own ? own_diag_tail(P.g) : 0);
   return {part, sc};
 }
 
@@ -265,7 +266,8 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
-                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local));
+                   reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
+                   nullptr, false, first + count == P.n_own ? std::min(count, own_diag_tail(P.g)) : 0);
 }
 
 // Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
@@ -479,7 +481,8 @@ void fwd_stats_sym(const at::Tensor& zq_local, const at::Tensor& zq_all, const a
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), tp + first, count,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
-                   reinterpret_cast<float2*>(part_x.data_ptr<float>()));
+                   reinterpret_cast<float2*>(part_x.data_ptr<float>()), false,
+                   first + count == P.n_own ? std::min(count, own_diag_tail(P.g)) : 0);
 }
 
 // Kept cosines of `tiles` -> own coefficient tiles in cbuf ([row_tiles][col_tiles] tiles) and the
@@ -843,6 +846,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("coef_gemm", &coef_gemm);
   m.def("dz", &dz);
   m.def("set_exp_backward", &set_exp_backward, py::arg("on"));
+  m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
+  m.def("diag_strips_enabled", &ntxent::diag_strips_enabled);
   m.def("exp_backward_enabled", &exp_backward_enabled);
   m.def("dz_exp", &dz_exp, py::arg("ebuf"), py::arg("zqt_all"), py::arg("lse2_all"), py::arg("plan"));
   m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"),

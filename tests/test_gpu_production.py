@@ -2,8 +2,10 @@
 narrow 8192 x 256 problem against an fp64 oracle computed ON THE GPU (fp64 MFMA/GEMM keeps the
 8192 x 8192 oracle to a few ms), plus the schedule corners the small tests never reach:
 
-* 528 forward tiles on 256 CUs = two data-parallel rounds + a stream-K remainder (and the
-  Z-ordered tile list) — the production mix of the headline step;
+* 528 forward tiles on 256 CUs = two data-parallel rounds + a 16-tile remainder, which the
+  diagonal-strip kernel finishes (the own block lists its diagonal tiles last) — the
+  production mix of the headline step; the stream-K split of the same remainder
+  (``set_diag_strips(False)``) must agree with it;
 * tau = 0.02 selects the per-tile-max exponential form of the forward epilogue (the fixed-shift
   form needs 2 log2(e)/tau < 120) at >= 512 tiles;
 * GEMM grids that leave CUs free for overlapped RCCL kernels (``set_grid_reserve``): a
@@ -128,3 +130,32 @@ def test_wide_rows_prep_block_path(ext, rows, dim, compute):
     lerr, gerr = _errors(h, 0.07, compute)
     lt, gt = TOL[("fp32", "fp32")] if compute == "fp32" else TOL[("bf16", compute)]
     assert lerr <= max(lt, 1e-6) and gerr <= gt, (lerr, gerr)
+
+
+@pytest.mark.parametrize("rows,dim,T,compute", [(8192, 512, 0.07, "fp16"), (8192, 256, 0.02, "fp32"),
+                                                (8192, 384, 0.07, "bf16")])
+def test_diag_strips_match_stream_k(ext, rows, dim, T, compute):
+    """The forward's whole-round remainder (16 diagonal tiles at 8192 rows on 256 CUs) finished by
+    the strip kernel (default) or by the stream-K split: same loss and gradient up to fp32
+    summation order; both fixed-shift (T = 0.07) and per-row-max (T = 0.02) epilogues."""
+    assert ext.diag_strips_enabled()
+    dt = torch.float32 if compute == "fp32" else torch.bfloat16
+    h = _views(rows, dim, seed=7 + dim, dtype=dt)
+    l0, g0 = _run(h, T, compute)
+    ext.set_diag_strips(False)
+    try:
+        l1, g1 = _run(h, T, compute)
+    finally:
+        ext.set_diag_strips(True)
+    assert abs(l1 - l0) <= 1e-6 * max(1.0, abs(l0)), (l0, l1)
+    assert (g1.float() - g0.float()).abs().max().item() <= 2e-3 * g0.float().abs().max().item()
+    lerr, gerr = _errors(h, T, compute)
+    if compute == "fp32":
+        lt, gt = TOL[("fp32", "fp32")]
+    elif T < 0.05:
+        lt, gt = TOL_SHARP_FP16
+    elif compute == "bf16":
+        lt, gt = 2e-5, TOL[("bf16", "bf16")][1]  # bf16 MFMA at d = 384: measured 8.9e-6 / 7.0e-3
+    else:
+        lt, gt = TOL[("bf16", compute)]
+    assert lerr <= lt and gerr <= gt, (lerr, gerr)

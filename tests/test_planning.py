@@ -57,6 +57,10 @@ def test_fwd_tiles_cover_once(C, rows, world, rank):
     assert set(covered.values()) == {1}
     rt = g["row_tiles"]
     assert len(tiles) == rt * (g["col_tiles"] - rt) + rt * (rt + 1) // 2
+    # the own block ends with its diagonal tiles (the strip kernel's remainder, launch_fwd_stats)
+    n_own = rt * (rt + 1) // 2
+    assert [t[2] for t in tiles[n_own - rt:n_own]] == [1] * rt
+    assert [t[0] for t in tiles[n_own - rt:n_own]] == list(range(rt))
 
 
 def test_dz_tiles_cover_output(C):

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Quick strip-kernel check: strips A/B test + rocprof of head/cfg2/cfg5 with and without strips.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-strips2}; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_production.py -m gpu -x -q -s -k "strips or headline" --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
+tail -1 $OUT/pytest.log
+prof() {  # tag, args
+  local t=$1; shift
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/p_$t -o run --output-format csv -- build/bin/ntxent_bench "$@" --iters 20 --warmup 3 > $OUT/$t.log 2>&1 || return 1
+  cp $(find $OUT/p_$t -name '*kernel_stats.csv' | head -1) $OUT/kstats_$t.csv
+  echo "$t: $(grep -A1 'fwd+bwd' $OUT/$t.log | tail -1 | cut -c1-150)"
+  grep -h "Li0ELi0ELi1E\|diag_strip" $OUT/kstats_$t.csv | cut -d, -f1,4 | sed 's/"_ZN6ntxent3dev//' | cut -c1-90
+}
+for c in "head --batch 4096 --dim 2048" "cfg2 --batch 4096 --dim 512" "cfg5 --batch 8192 --dim 1024 --compute fp16"; do
+  set -- $c; t=$1; shift
+  prof ${t} "$@" && prof ${t}_nostrips "$@" --no-strips || exit 1
+done
+for i in 1 2; do
+timeout -k 10 200 python bench.py > $OUT/bench$i.log 2>&1 || { echo "bench failed"; tail $OUT/bench$i.log; exit 1; }
+tail -1 $OUT/bench$i.log | cut -c1-250
+done
+echo done
