@@ -78,6 +78,10 @@ def parse(argv=None):
     ap.add_argument("--secondary-fp32", default="auto", choices=["auto", "on", "off"],
                     help="also time the exact-fp32 MFMA path (fp32 inputs, fp32 compute) at the same shape "
                          "(auto: on for 1 GPU)")
+    ap.add_argument("--prewarm-steps", type=int, default=60,
+                    help="untimed steps run BEFORE the --warmup steps so the timed region measures the "
+                         "steady state: from a cold start the GPU clock ramps for ~60 steps (0.51 ms/step "
+                         "at steps 10-19, 0.44 from step 60 on: profiles/r2/ramp); reported in the JSON")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="launcher: seconds before the whole job is killed; ranks: process-group timeout")
     ap.add_argument("--json-out", default=None)
@@ -293,9 +297,18 @@ def run_rank(a) -> None:
             graph.replay()
             return g_loss, g_gh
 
+    prewarm = max(0, a.prewarm_steps) if on_gpu else 0
+    for _ in range(prewarm):  # same count on every rank (each step runs collectives)
+        step()
     if on_gpu:
         torch.cuda.reset_peak_memory_stats(dev)
-    dt_s, per_ms, comm_ms, loss, gh = timed(step, a.steps, a.warmup, comm=world > 1)
+    # The timed region has no per-step events (a timing event recorded between two steps left a
+    # ~5-8 us bubble per step in the kernel trace); the per-step distribution comes from a
+    # separate pass right after it.
+    dt_s, _, comm_ms, loss, gh = timed(step, a.steps, a.warmup, per_step_events=False, comm=world > 1)
+    per_ms = None
+    if on_gpu:
+        _, per_ms, _, _, _ = timed(step, min(a.steps, 20), 0, per_step_events=True)
     peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20 if on_gpu else None
     lossv = float(loss.item())
     finite = bool(lossv == lossv and torch.isfinite(gh).all().item())
@@ -376,7 +389,13 @@ def run_rank(a) -> None:
                 "hip_graph": bool(a.graph),
                 "device": a.device,
             },
+            "prewarm_steps": prewarm,
+            "prewarm_note": ("untimed steps before the warmup steps: the GPU clock ramps over the first "
+                             "~60 steps after a cold start (profiles/r2/ramp); the timed region is the "
+                             "steady state") if prewarm else None,
             "step_ms": _stats(per_ms) if per_ms else None,
+            "step_ms_source": ("HIP events around each of %d steps, a separate pass after the timed region"
+                               % min(a.steps, 20)) if per_ms else None,
             "peak_hbm_mb": round(peak_mb, 1) if peak_mb is not None else None,
             "peak_hbm_mb_per_rank": [round(x, 1) for x in peak_all] if peak_all else None,
             "comm_wait_ms_per_step": {k: round(v, 4) for k, v in comm_ms.items()} if comm_ms else None,

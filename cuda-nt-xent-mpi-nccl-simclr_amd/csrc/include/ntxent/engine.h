@@ -122,6 +122,7 @@ class Engine {
   GemmWorkspace ws_;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_prep_ = nullptr, ev_zq_ = nullptr, ev_zqt_ = nullptr;
+
   bool zqt_pending_ = false;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;

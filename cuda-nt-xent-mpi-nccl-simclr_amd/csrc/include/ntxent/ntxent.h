@@ -190,7 +190,8 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
                       const BlockView& bv = BlockView{}, float2* part_x = nullptr, bool store_exp = false,
-                      int diag_tail = 0);
+                      int diag_tail = 0, hipEvent_t main_done = nullptr);
+// main_done (optional): recorded on `stream` right after the persistent GEMM, before the strips.
 // Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
 void set_diag_strips(bool on);
 bool diag_strips_enabled();
@@ -216,8 +217,11 @@ void launch_dz_exp(DType comp, const void* ebuf, const void* zqt_all, const floa
 // lse_scratch_floats(g) floats that must be ZERO when first used (the kernel leaves it
 // reusable: its arrival counter returns to zero).
 int lse_scratch_floats(const Geometry& g);
+// zq / zqt (optional, rank-local [Rpad, ld_k] rows in tr_dtype): the same launch also writes the
+// transpose zqt = zq^T (launch_transpose) from extra blocks that run beside the merge.
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos,
-                float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream);
+                float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream,
+                DType tr_dtype = DType::F16, const void* zq = nullptr, void* zqt = nullptr);
 
 // Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
 // `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;

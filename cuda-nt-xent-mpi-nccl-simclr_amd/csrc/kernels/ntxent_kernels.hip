@@ -362,12 +362,11 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
 // 64x64 tile transpose with 16-byte global accesses on both sides (rows of Zq in, rows of
 // ZqT out); the LDS tile is padded by 16 B per row.
 template <typename T>
-__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
-                                                        int dk, int ldk, int ldt) {
+__device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __restrict__ zqt, int dk, int ldk, int ldt,
+                                               int bx, int by, T (&tile)[64][64 + 16 / sizeof(T)]) {
   constexpr int V = 16 / sizeof(T);  // elements per 16 B
   constexpr int CPR = 64 / V;        // 16-B chunks per 64-element row
-  __shared__ __attribute__((aligned(16))) T tile[64][64 + V];
-  const int j0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+  const int j0 = bx * 64, e0 = by * 64;
   for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
     const int r = k / CPR, c = k % CPR;
     u32x4 v = {0u, 0u, 0u, 0u};
@@ -382,6 +381,13 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
     for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][er];
     *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
+                                                        int dk, int ldk, int ldt) {
+  __shared__ __attribute__((aligned(16))) T tile[64][64 + 16 / sizeof(T)];
+  transpose_tile<T>(zq, zqt, dk, ldk, ldt, blockIdx.x, blockIdx.y, tile);
 }
 
 // Row statistics from a row's merged negatives-only (max, sum) state: returns lse2 and writes
@@ -402,13 +408,24 @@ __device__ __forceinline__ float finish_row(float m, float s, float yp, float& l
 // cancellation). Pad rows [R, Rpad) get zeros. One thread per pair left the chip ~94% idle
 // (16 workgroups for B = 4096) and serialised 32-64 dependent merges per thread.
 constexpr int kLseLanes = 8;
-__global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ part, const float* __restrict__ ypos,
-                                                  float* __restrict__ lse2_all, float* __restrict__ cpos,
-                                                  float* __restrict__ block_loss, float* __restrict__ loss_sum,
-                                                  float loss_scale, int R, int Rpad, int Tc, int own0) {
-  __shared__ float red[16];
+struct LseArgs {
+  const float2* part;
+  const float* ypos;
+  float* lse2_all;
+  float* cpos;
+  float* block_loss;
+  float* loss_sum;
+  float loss_scale;
+  int R, Rpad, Tc, own0;
+};
+// Block `bid` of the nb LSE blocks (the last of them to finish sums the loss).
+__device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, float* red, int& last) {
+  const float2* __restrict__ part = a.part;
+  const int R = a.R, Rpad = a.Rpad, Tc = a.Tc, own0 = a.own0;
+  float* __restrict__ lse2_all = a.lse2_all;
+  float* __restrict__ cpos = a.cpos;
   const int n = R >> 1;
-  const int gt = blockIdx.x * 256 + threadIdx.x;
+  const int gt = bid * 256 + threadIdx.x;
   const int item = gt / kLseLanes, q = gt % kLseLanes;
   float li = 0.f;
   if (item < n) {  // uniform across the 8 lanes of an item
@@ -438,7 +455,7 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
       lse_merge(mj, sj, __shfl_xor(mj, off), __shfl_xor(sj, off));
     }
     if (q == 0) {
-      const float yp = ypos[i];
+      const float yp = a.ypos[i];
       float l_i, l_j, a_i, a_j;
       lse2_all[own0 + i] = finish_row(mi, si, yp, l_i, a_i);
       lse2_all[own0 + j] = finish_row(mj, sj, yp, l_j, a_j);
@@ -458,23 +475,46 @@ __global__ __launch_bounds__(256) void lse_kernel(const float2* __restrict__ par
   // write-through (sc1) 4-byte store and the last block reads the partials with sc1 loads,
   // so no agent release/acquire is needed (MI355X_MICROARCH.md § visibility, Valid forms
   // row 1); a release fence here wrote back every dirty L2 line the forward GEMM left behind.
-  __shared__ int last;
-  int* cnt = reinterpret_cast<int*>(block_loss);  // fixed slot 0: the counter
-  float* partial = block_loss + 64;               // per-block partials after it
+  int* cnt = reinterpret_cast<int*>(a.block_loss);  // fixed slot 0: the counter
+  float* partial = a.block_loss + 64;               // per-block partials after it
   if (threadIdx.x == 0) {
-    __hip_atomic_store(partial + blockIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(partial + bid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == (int)gridDim.x - 1;
+    last = old == nb - 1;
     if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (last && threadIdx.x < 64) {
     float s = 0.f;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += 64)
+    for (int b = threadIdx.x; b < nb; b += 64)
       s += __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s = wave_sum(s);  // fixed lane assignment and tree: deterministic
-    if (threadIdx.x == 0) loss_sum[0] = s * loss_scale;
+    if (threadIdx.x == 0) a.loss_sum[0] = s * a.loss_scale;
+  }
+}
+
+__global__ __launch_bounds__(256) void lse_kernel(const LseArgs a) {
+  __shared__ float red[16];
+  __shared__ int last;
+  lse_block(a, blockIdx.x, gridDim.x, red, last);
+}
+
+// The LSE merge and the Z -> Z^T transpose (the dZ GEMM's B operand) in one launch: blocks
+// [0, nb) merge, the rest transpose one 64x64 tile each. The merge is latency-bound on few
+// blocks and the transpose is bandwidth-bound on many, so they share the chip instead of
+// running back to back, and no side stream / event join (a ~5-7 us bubble each) is needed.
+template <typename T>
+__global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int nb, const T* __restrict__ zq,
+                                                            T* __restrict__ zqt, int dk, int ldk, int ldt, int tx) {
+  __shared__ __attribute__((aligned(16))) T tile[64][64 + 16 / sizeof(T)];
+  __shared__ float red[16];
+  __shared__ int last;
+  if ((int)blockIdx.x < nb) {
+    lse_block(a, blockIdx.x, nb, red, last);
+  } else {
+    const int t = blockIdx.x - nb;
+    transpose_tile<T>(zq, zqt, dk, ldk, ldt, t % tx, t / tx, tile);
   }
 }
 
@@ -1052,7 +1092,8 @@ bool diag_strips_enabled() { return g_diag_strips.load(); }
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp, int diag_tail) {
+                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp, int diag_tail,
+                      hipEvent_t main_done) {
   if (ntiles == 0) return;
   NTXENT_CHECK(diag_tail >= 0 && diag_tail <= ntiles, "fwd_stats: bad diagonal tail");
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
@@ -1087,6 +1128,7 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
+    if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
       if (nstrip > 0) {
         NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diag strips: row-major operands only");
@@ -1140,10 +1182,21 @@ static int lse_blocks(const Geometry& g) { return ((g.rows_pad - g.rows / 2) * d
 int lse_scratch_floats(const Geometry& g) { return 64 + lse_blocks(g); }  // counter slot + partials
 
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
-                float* loss_sum, const Geometry& g, hipStream_t stream) {
+                float* loss_sum, const Geometry& g, hipStream_t stream, DType tr_dtype, const void* zq, void* zqt) {
   const int nb = lse_blocks(g);  // one workgroup per 32 pairs / pad rows
-  hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, part, ypos, lse2_all, cpos, block_loss, loss_sum,
-                     (float)(1.0 / (double)g.global_rows), g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad);
+  dev::LseArgs a{part, ypos, lse2_all, cpos, block_loss, loss_sum, (float)(1.0 / (double)g.global_rows),
+                 g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad};
+  if (zq == nullptr) {
+    hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, a);
+  } else {
+    NTXENT_CHECK(zqt != nullptr, "lse: transpose output missing");
+    const int tx = g.rows_pad / 64, ty = g.dim_n / 64;
+    dispatch_comp(tr_dtype, [&](auto tc) {
+      using Tc = decltype(tc);
+      hipLaunchKernelGGL((dev::lse_transpose_kernel<Tc>), dim3(nb + tx * ty), dim3(256), 0, stream, a, nb,
+                         static_cast<const Tc*>(zq), static_cast<Tc*>(zqt), g.dim_k, g.ld_k, g.ld_t, tx);
+    });
+  }
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 

@@ -126,7 +126,8 @@ void Engine::forward(const void* h, hipStream_t s) {
       if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
       return;
     }
-    launch_transpose(bwd_, zq_local, zqt_local, g_, s);
+    // world 1: the transpose is written by the LSE launch (beside the merge, see below)
+    if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
@@ -158,7 +159,8 @@ void Engine::forward(const void* h, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.lse");
     fault_point("lse");
-    launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
+    if (world_ == 1) launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
+    else launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
   }
   if (world_ > 1) {
     NTXENT_TRACE("ntxent.lse_gather");

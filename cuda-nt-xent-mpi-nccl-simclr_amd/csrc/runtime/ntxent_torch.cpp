@@ -224,7 +224,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
 }
 
 std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P,
-                                  bool keep_cos, bool store_exp = false) {
+                                  bool keep_cos, bool store_exp = false, hipEvent_t main_done = nullptr) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.op_ld(),
@@ -241,7 +241,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), sc.defined() ? sc.data_ptr() : nullptr,
                    ws, P.g, cur_stream(zq_local), BlockView{}, nullptr, store_exp,
-                   P.n_fwd == P.n_own ? own_diag_tail(P.g) : 0);
+                   P.n_fwd == P.n_own ? own_diag_tail(P.g) : 0, main_done);
   return {part, sc};
 }
 
@@ -273,7 +273,8 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
 // Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
 // -(a_i + a_p) of the local rows); returns the local loss contribution.
 at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_all, at::Tensor& cpos,
-               const Plan& P) {
+               const Plan& P, const c10::optional<at::Tensor>& zq = c10::nullopt,
+               const c10::optional<at::Tensor>& zqt = c10::nullopt) {
   check_input(part, "part");
   NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad && lse2_all.scalar_type() == at::kFloat,
                "lse2_all must be float32 [world*rows_pad]");
@@ -281,9 +282,20 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
   const at::DeviceGuard guard(part.device());
   auto block_loss = device_scratch(part, (size_t)lse_scratch_floats(P.g) * 4, 1);
   auto loss = at::empty({}, opts(part, at::kFloat));
+  const bool tr = zq.has_value() && zq->defined();
+  if (tr) {  // also write zqt = zq^T (the rank-local rows) from the same launch
+    NTXENT_CHECK(zqt.has_value() && zqt->defined(), "lse: zqt missing");
+    check_input(*zq, "zq");
+    check_input(*zqt, "zqt");
+    NTXENT_CHECK(zq->numel() == (long)P.g.rows_pad * P.g.ld_k && zq->scalar_type() == to_scalar(P.bwd()),
+                 "lse: zq must be [rows_pad, ld_k] in the backward dtype");
+    NTXENT_CHECK(zqt->numel() == (long)P.g.dim_n * P.g.ld_t && zqt->scalar_type() == zq->scalar_type(),
+                 "lse: zqt must be [dim_n, ld_t]");
+  }
   launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(),
              lse2_all.data_ptr<float>(), cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()),
-             loss.data_ptr<float>(), P.g, cur_stream(part));
+             loss.data_ptr<float>(), P.g, cur_stream(part), P.bwd(), tr ? zq->data_ptr() : nullptr,
+             tr ? zqt->data_ptr() : nullptr);
   return loss;
 }
 
@@ -628,32 +640,10 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
                      cur_stream(h));
     return {loss, pr[0], at::Tensor(), pr[1], lse2, at::Tensor(), arow};
   }
-  // ZqT (the dZ GEMM's B operand) is first read in the backward: the transpose runs on a side
-  // stream beside the forward GEMM, whose blocks (one per CU, 128 KiB LDS) leave LDS and
-  // memory bandwidth for it, and the current stream joins it after the LSE kernel.
-  const auto dev = h.device().index();
-  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev);
-  // one side stream per device and thread (a fresh pool stream per call paid a new HW queue
-  // on each of the pool's first 32 uses)
-  thread_local std::map<int, c10::hip::HIPStreamMasqueradingAsCUDA> sides;
-  auto sit = sides.find(dev);
-  if (sit == sides.end()) sit = sides.emplace(dev, c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, dev)).first;
-  const auto side = sit->second;
-  thread_local std::map<int, std::pair<hipEvent_t, hipEvent_t>> evs;
-  auto& ev = evs[dev];
-  if (!ev.first) {
-    // device-scope events: a system-scope release fence per record left ~6-10 us bubbles
-    const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev.first, fl));
-    NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev.second, fl));
-  }
+  // ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes it from
+  // extra blocks beside the merge (one stream: a side-stream transpose cost an event record and
+  // a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
   auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
-  NTXENT_HIP_CHECK(hipEventRecord(ev.first, cur.stream()));
-  NTXENT_HIP_CHECK(hipStreamWaitEvent(side.stream(), ev.first, 0));
-  launch_transpose(P->bwd(), pr[0].data_ptr(), zqt.data_ptr(), P->g, side.stream());
-  NTXENT_HIP_CHECK(hipEventRecord(ev.second, side.stream()));
-  c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(pr[0].storage().data_ptr(), side);
-  c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(zqt.storage().data_ptr(), side);
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
@@ -663,8 +653,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true, ex) : fwd_stats(pr[0], pr[0], *P, keep, keep && ex);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-  auto loss = lse(fs[0], pr[2], lse2, cpos, *P);
-  NTXENT_HIP_CHECK(hipStreamWaitEvent(cur.stream(), ev.second, 0));
+  auto loss = lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
@@ -839,9 +828,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"));
-  m.def("fwd_stats", &fwd_stats, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"),
-        py::arg("store_exp") = false);
-  m.def("lse", &lse);
+  m.def("fwd_stats",
+        [](const at::Tensor& zl, const at::Tensor& za, const Plan& P, bool keep, bool ex) {
+          return fwd_stats(zl, za, P, keep, ex);
+        },
+        py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"), py::arg("store_exp") = false);
+  m.def("lse", &lse, py::arg("part"), py::arg("ypos"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
+        py::arg("zq") = py::none(), py::arg("zqt") = py::none());
   m.def("coef", &coef);
   m.def("coef_gemm", &coef_gemm);
   m.def("dz", &dz);
