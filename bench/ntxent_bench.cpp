@@ -347,6 +347,7 @@ int main(int argc, char** argv) {
     else if (a == "--recompute") o.recompute = true;
     else if (a == "--no-small") o.small = false;
     else if (a == "--no-strips") ntxent::set_diag_strips(false);
+    else if (a == "--no-splitk") ntxent::set_splitk_reduce(false);
     else if (a == "--exp") g_exp_backward = true;
     else if (a == "--no-exp") g_exp_backward = false;
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
@@ -355,6 +356,7 @@ int main(int argc, char** argv) {
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
                   "                    [--recompute] [--no-small] [--gpus N] [--json out.json]\n"
                   "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n"
+                  "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"
                   "  --no-strips: forward remainder tiles by the stream-K split instead of diagonal strips (A/B)\n"
                   "  --exp / --no-exp: coefficient-free backward (exponential store, C formed in the dZ GEMM) or\n"
                   "                    the coefficient pass + dZ GEMM (default)\n");

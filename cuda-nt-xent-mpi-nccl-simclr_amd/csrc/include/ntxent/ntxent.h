@@ -195,6 +195,12 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
 // Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
 void set_diag_strips(bool on);
 bool diag_strips_enabled();
+// Split-K forward for own-block launches with fewer tiles than CUs and long K (on by default;
+// off = the stream-K schedule's serial last-arriver fixup, for A/B): K pieces of every tile
+// publish fp32 partial slabs and a second launch sums them and runs the epilogue in strips.
+void set_splitk_reduce(bool on);
+bool splitk_reduce_enabled();
+int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
 
 // ---- coefficient-free backward ---------------------------------------------------------------
 // Plans whose forward can keep exponentials for it: reduced precision, fixed-shift epilogue

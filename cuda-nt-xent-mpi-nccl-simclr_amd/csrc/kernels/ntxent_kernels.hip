@@ -1002,9 +1002,11 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
 // fixed size so that launches of different tile counts sharing one workspace never place
 // their fp32 partial slabs over another launch's (self-cleaning, zero) counters.
 
+// + the split-K forward's column-partial strips (fewer tiles than CUs: < num_cus tiles).
 size_t gemm_workspace_bytes(int ntiles, int num_cus) {
   (void)ntiles;
-  return sk_counter_bytes(num_cus) + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float);
+  return sk_counter_bytes(num_cus) + (size_t)2 * std::max(1, num_cus) * kTileElems * sizeof(float) +
+         (size_t)std::max(1, num_cus) * dev::kSkColpTile * sizeof(float2);
 }
 
 std::vector<int4> build_dz_tiles(const Geometry& g) {
@@ -1089,6 +1091,18 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 static std::atomic<bool> g_diag_strips{true};
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
+static std::atomic<bool> g_splitk_reduce{true};
+void set_splitk_reduce(bool on) { g_splitk_reduce = on; }
+bool splitk_reduce_enabled() { return g_splitk_reduce.load(); }
+
+// K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
+// than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
+// partial slabs serially (BASELINE config 4: 36 tiles x 128 K-steps, fixup ~40 % of the GEMM).
+int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
+  if (!splitk_reduce_enabled() || diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
+  const int pcs = std::min(cus / ntiles, nk / 8);
+  return pcs >= 2 ? pcs : 0;
+}
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
@@ -1118,16 +1132,40 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   // strips (diag_strip_kernel) after it instead of as a third round / stream-K split. fp8 and
   // exponential-store launches keep the stream-K schedule.
   int nstrip = 0;
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
   if (diag_tail > 0 && comp != DType::FP8 && !store_exp && diag_strips_enabled()) {
-    const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
     const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
     if (q >= 1 && rem > 0 && rem <= diag_tail) nstrip = rem;
   }
   const int nmain = ntiles - nstrip;
-  const int grid = apply_schedule(p, nmain, ws, stream);
+  const int nk_tile = (int)(kb / kKStepBytes);
+  const int pieces = (!store_exp && part_x == nullptr) ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
+  int grid;
+  if (pieces > 0) {  // split-K: every piece publishes its slab, sk_reduce_kernel finishes the tiles
+    NTXENT_CHECK(kb % kKStepBytes == 0, "K not aligned to the K step");
+    p.nk = nk_tile;
+    p.dp_tiles = 0;
+    p.sk_tiles = ntiles;
+    p.ipb = (nk_tile + pieces - 1) / pieces;
+    p.sk_out = 1;
+    p.sk_cnt = static_cast<int*>(ws.ptr);
+    p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+    grid = (int)(((long long)ntiles * nk_tile + p.ipb - 1) / p.ipb);
+    NTXENT_CHECK(grid <= ws.num_cus && ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
+                 "split-K forward: workspace too small");
+  } else {
+    grid = apply_schedule(p, nmain, ws, stream);
+  }
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
+    if (pieces > 0) {
+      using TS = typename dev::StoreT<Tc>::type;
+      float2* colp = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
+                                               (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
+      if (p.fixed_shift) hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 1>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp);
+      else hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 0>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp);
+    }
     if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
       if (nstrip > 0) {

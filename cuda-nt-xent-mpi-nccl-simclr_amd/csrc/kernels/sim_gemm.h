@@ -103,6 +103,8 @@ struct SimParams {
   long long ipb;         // stream-K K-steps per block
   float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
   int* sk_cnt;           // [sk_tiles] arrival counters (zero at launch; self-cleaning)
+  int sk_out;            // forward split-K: every piece only publishes its slab; sk_reduce_kernel
+                         // sums a tile's slabs and runs its epilogue in row / column strips
 };
 
 // Kept-cosine layout for 2-byte types: one 16-byte unit per lane holds the fragments of the
@@ -894,6 +896,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
+    if (p.sk_out) {  // split-K forward: the reduce launch finishes the tile
+      tstamp(8 + 6 * item);
+      continue;
+    }
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1413,6 +1419,161 @@ __global__ __launch_bounds__(256) void diag_strip_kernel(const SimParams p) {
     for (int q = 1; q < 4; ++q) lse_merge(m, s, red[2 * (q * 16 + i)], red[2 * (q * 16 + i) + 1]);
     p.part[(long long)nt * p.Rpad + r0 + rb0 + i] = make_float2(m, s);
   }
+}
+
+// ------------------------------------------------------------------------------------
+// Split-K forward for tile-starved launches (fewer tiles than CUs, long K: BASELINE config 4,
+// 36 tiles x 128 K-steps): every K piece of the persistent GEMM publishes its fp32 partial tile
+// (sk_out), and this launch sums each tile's pieces (fixed block order: deterministic) and runs
+// the forward epilogue in 16 row strips per tile instead of one last-arriving block per tile
+// reading all p - 1 slabs serially. A strip block writes its rows' partials (complete over the
+// tile) and the kept cosines; for a kTileSymOff tile it also publishes its 16-row column
+// partials (sc1 stores into colp), and the tile's last strip block to arrive (ticket) merges
+// the 16 strips per column in strip order. A slab holds the tile in the GEMM's fragment order:
+// float ((w * 32 + f) * 64 + lane) * 4 + r for wave w, fragment f = 4 mi + ni.
+// ------------------------------------------------------------------------------------
+constexpr int kSkColpTile = 16 * kTile;  // float2 column partials per tile: [16 strips][256 cols]
+
+__device__ __forceinline__ int sk_frag_off(int row, int col) {  // float offset of element (row, col)
+  const int mi = 4 * (row >> 7) + ((row >> 4) & 3), wa = (row >> 6) & 1;
+  const int ni = 2 * (col >> 7) + ((col >> 4) & 1), wb = (col >> 5) & 3;
+  const int lane = 16 * ((row >> 2) & 3) + (col & 15);
+  return (((4 * wa + wb) * 32 + 4 * mi + ni) * 64 + lane) * 4 + (row & 3);
+}
+
+template <typename TS, int FX>
+__global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float2* __restrict__ colp) {
+  __shared__ float red[4][16][2];
+  __shared__ int last_flag;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile = blockIdx.x >> 4, strip = blockIdx.x & 15;
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y, kind = t.z;
+  const int s16 = 16 * strip;
+  const int nk = p.nk;
+  const long long ipb = p.ipb;
+  const int b0 = (int)((long long)tile * nk / ipb), b1 = (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  // this thread's 4 fragments (s16, cb[j] = 64 w + 16 j), MFMA C layout: rows s16 + r4 + r,
+  // column cb[j] + c1; a wave reads 1 KiB contiguous per fragment and slab
+  const int r4 = 4 * (lane >> 4), c1 = lane & 15;
+  int off[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) off[j] = sk_frag_off(s16 + r4, 64 * w + 16 * j + c1);
+  f32x4 v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
+  auto slab = [&](int bb) {
+    const long long st = (long long)bb * ipb;
+    const bool first_partial = (st / nk == tile) && (st % nk != 0);
+    return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
+  };
+  // 4 slabs per round, all 16 loads issued before the adds (clamped indices: no conditional
+  // load; a clamped duplicate is multiplied by 0)
+  for (int bb = b0; bb <= b1; bb += 4) {
+    f32x4 x[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float* sl = slab(bb + u <= b1 ? bb + u : b1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[u][j] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(sl + off[j]));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float k = bb + u <= b1 ? 1.f : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += x[u][j] * k;
+    }
+  }
+  if (p.sc) {  // kept cosines (canonical fragment order), before the masks
+    TS* st = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
+    const float cs = p.cos_scale;
+    if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+      for (int np = 0; np < 2; ++np) {
+        union { TS h[8]; u32x4 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pk.h[r] = from_f32<TS>(v[2 * np][r] * cs);
+          pk.h[4 + r] = from_f32<TS>(v[2 * np + 1][r] * cs);
+        }
+        *reinterpret_cast<u32x4*>(st + sc_unit(s16, 64 * w + 32 * np, lane) * 8) = pk.u;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(st + (((s16 >> 4) * 16 + ((64 * w + 16 * j) >> 4)) * 64 + lane) * 4) = v[j] * cs;
+    }
+  }
+  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
+  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+  const float sc_ = p.acc_scale, M = p.y_scale;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tr = s16 + r4 + r, tc = 64 * w + 16 * j + c1, gi = r0 + tr, d = tc - tr;
+      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
+                        ((d == D2) & (gi >= p.n_half));
+      v[j][r] = drop ? kNegInf : v[j][r] * sc_;
+    }
+  // row partials over this wave's 64 columns (the 16 lanes of a DPP row), merged over the waves
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float m = M;
+    if constexpr (!FX) m = row16_max(fmaxf(fmaxf(v[0][r], v[1][r]), fmaxf(v[2][r], v[3][r])));
+    const float ms = (m == kNegInf) ? 0.f : m;
+    float sr = (fast_exp2(v[0][r] - ms) + fast_exp2(v[1][r] - ms)) + (fast_exp2(v[2][r] - ms) + fast_exp2(v[3][r] - ms));
+    sr = row16_sum(sr);
+    if (c1 == 0) {
+      red[w][r4 + r][0] = FX ? (sr > 0.f ? M : kNegInf) : m;
+      red[w][r4 + r][1] = sr;
+    }
+  }
+  const bool sym = kind == kTileSymOff;
+  if (sym) {  // this strip's column partials (16 rows): the 4 rows of a lane, lanes l ^ 16, 32, 48
+    const auto crs = __builtin_amdgcn_make_buffer_rsrc(colp + (size_t)tile * kSkColpTile, 0, kSkColpTile * 8, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float m = M;
+      if constexpr (!FX) m = xrow_max(fmaxf(fmaxf(v[j][0], v[j][1]), fmaxf(v[j][2], v[j][3])));
+      const float ms = (m == kNegInf) ? 0.f : m;
+      float sc2 = (fast_exp2(v[j][0] - ms) + fast_exp2(v[j][1] - ms)) + (fast_exp2(v[j][2] - ms) + fast_exp2(v[j][3] - ms));
+      sc2 = xrow_sum(sc2);
+      const float mo = FX ? (sc2 > 0.f ? M : kNegInf) : m;
+      if (lane < 16)  // write-through (sc1): read by the tile's last strip block on any XCD
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mo), __float_as_uint(sc2)}, crs,
+                                              (strip * kTile + 64 * w + 16 * j + c1) * 8, 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int i = threadIdx.x;
+    float m = red[0][i][0], s = red[0][i][1];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) lse_merge(m, s, red[q][i][0], red[q][i][1]);
+    p.part[(long long)nt * p.Rpad + r0 + s16 + i] = make_float2(m, s);
+  }
+  if (!sym) return;
+  if (threadIdx.x == 0) {  // ticket: the 16th strip block of the tile merges the column partials
+    const int old = __hip_atomic_fetch_add(p.sk_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == 15;
+    if (last) __hip_atomic_store(p.sk_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  const auto crs = __builtin_amdgcn_make_buffer_rsrc(colp + (size_t)tile * kSkColpTile, 0, kSkColpTile * 8, 0x00020000);
+  const int c = threadIdx.x;  // one column per thread, strips in order (deterministic)
+  u32x2 q[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b64(crs, (k * kTile + c) * 8, 0, 16);
+  float m = __uint_as_float(q[0][0]), s = __uint_as_float(q[0][1]);
+#pragma unroll
+  for (int k = 1; k < 16; ++k) lse_merge(m, s, __uint_as_float(q[k][0]), __uint_as_float(q[k][1]));
+  p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
 }
 
 }  // namespace dev

@@ -840,6 +840,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dz", &dz);
   m.def("set_exp_backward", &set_exp_backward, py::arg("on"));
   m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
+  m.def("set_splitk_reduce", &ntxent::set_splitk_reduce, py::arg("on"));
+  m.def("splitk_reduce_enabled", &ntxent::splitk_reduce_enabled);
+  m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
+        py::arg("diag_tail"));
   m.def("diag_strips_enabled", &ntxent::diag_strips_enabled);
   m.def("exp_backward_enabled", &exp_backward_enabled);
   m.def("dz_exp", &dz_exp, py::arg("ebuf"), py::arg("zqt_all"), py::arg("lse2_all"), py::arg("plan"));

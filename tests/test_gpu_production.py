@@ -159,3 +159,35 @@ def test_diag_strips_match_stream_k(ext, rows, dim, T, compute):
     else:
         lt, gt = TOL[("bf16", compute)]
     assert lerr <= lt and gerr <= gt, (lerr, gerr)
+
+
+@pytest.mark.parametrize("rows,dim,T,compute", [(2048, 8192, 0.07, "fp16"), (2048, 4096, 0.02, "fp32"),
+                                                (1000, 6000, 0.07, "bf16")])
+def test_splitk_reduce_matches_stream_k(ext, rows, dim, T, compute):
+    """Tile-starved forward (BASELINE config 4: 36 tiles x 128 K-steps on 256 CUs): the split-K
+    pieces + strip-parallel reduce (default) against the stream-K last-arriver fixup, and both
+    against the fp64 oracle; fixed-shift and per-row-max epilogues, padded rows (1000)."""
+    nk = (dim + 63) // 64 * 64 * (4 if compute == "fp32" else 2) // 128
+    rt = (rows + 255) // 256
+    ntiles = rt * (rt + 1) // 2
+    assert ext.splitk_reduce_enabled()
+    assert ext.fwd_splitk_pieces(ntiles, nk, ext.device_info(0)["num_cus"], rt) >= 2
+    dt = torch.float32 if compute == "fp32" else torch.bfloat16
+    h = _views(rows, dim, seed=11 + dim, noise=2.0, dtype=dt)  # noisy views: O(1) loss
+    l0, g0 = _run(h, T, compute)
+    ext.set_splitk_reduce(False)
+    try:
+        l1, g1 = _run(h, T, compute)
+    finally:
+        ext.set_splitk_reduce(True)
+    assert abs(l1 - l0) <= 1e-6 * max(1.0, abs(l0)), (l0, l1)
+    # summation order of the K pieces differs: a few output ulps (bf16 gradient)
+    assert (g1.float() - g0.float()).abs().max().item() <= 1e-2 * g0.float().abs().max().item()
+    lerr, gerr = _errors(h, T, compute)
+    if compute == "fp32":
+        lt, gt = TOL[("fp32", "fp32")]
+    elif compute == "bf16":
+        lt, gt = 2e-5, TOL[("bf16", "bf16")][1]
+    else:
+        lt, gt = TOL[("bf16", compute)]
+    assert lerr <= max(lt, 1e-6) and gerr <= gt, (lerr, gerr)
