@@ -198,6 +198,10 @@ bool diag_strips_enabled();
 // Split-K forward for own-block launches with fewer tiles than CUs and long K (on by default;
 // off = the stream-K schedule's serial last-arriver fixup, for A/B): K pieces of every tile
 // publish fp32 partial slabs and a second launch sums them and runs the epilogue in strips.
+// Coefficient pass row-major stores from lane-permuted registers (one row per 4-lane quad; on by
+// default, off for A/B).
+void set_coef_lane_permute(bool on);
+bool coef_lane_permute();
 void set_splitk_reduce(bool on);
 bool splitk_reduce_enabled();
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);

@@ -1091,6 +1091,9 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 static std::atomic<bool> g_diag_strips{true};
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
+static std::atomic<bool> g_coef_perm{true};
+void set_coef_lane_permute(bool on) { g_coef_perm = on; }
+bool coef_lane_permute() { return g_coef_perm.load(); }
 static std::atomic<bool> g_splitk_reduce{true};
 void set_splitk_reduce(bool on) { g_splitk_reduce = on; }
 bool splitk_reduce_enabled() { return g_splitk_reduce.load(); }
@@ -1251,7 +1254,8 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
   p.cpos = cpos;
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(16 * ntiles), dim3(64), 0, stream, p);
+    if (coef_lane_permute()) hipLaunchKernelGGL((dev::coef_kernel<Tc, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
+    else hipLaunchKernelGGL((dev::coef_kernel<Tc, false>), dim3(16 * ntiles), dim3(64), 0, stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

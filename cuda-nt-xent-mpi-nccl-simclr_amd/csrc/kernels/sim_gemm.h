@@ -150,7 +150,7 @@ struct KStream {
 // staged transposed in LDS, then written row-major into slot (mt, nt) with 16-B stores
 // (rows via ds_read_b64_tr_b16) and, for a mirrored tile, into the lower-triangular slot.
 // ------------------------------------------------------------------------------------
-template <typename T, int NW, int NMI = 8>
+template <typename T, int NW, int NMI = 8, bool PERM = true>
 __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&rb)[NMI], const int (&cb)[4],
                                               int row_base, int col_base, int mt, int nt, int kind,
                                               lds_char* lds, const SimParams& p, int lane) {
@@ -260,8 +260,20 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
       u[2] = (unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
       u[3] = (unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
-      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
-                                (col_base + r0) * 2) = u;
+      if constexpr (PERM) {
+        // lanes i + 16 g hold 16-byte chunk g of row c0 + i: permute so that lane 4 i + g holds it,
+        // and each 4-lane quad stores one contiguous 64-byte row segment (one row per quad
+        // instead of four: a quad spanning four rows cost the store path ~4x its cycles)
+        const int src = ((lane >> 2) + 16 * (lane & 3)) << 2;
+        u32x4 v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)u[k]);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + (lane >> 2)) * (kTile * 2) +
+                                  (col_base + (blk / RB) * 32 + 8 * (lane & 3)) * 2) = v;
+      } else {
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
+                                  (col_base + r0) * 2) = u;
+      }
     }
   }
 }
@@ -1228,7 +1240,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 // (canonical fragment order: 16 fragments of 512 B) -> C into the coefficient buffer. 9 KiB of
 // LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound), and 16
 // waves per tile keep a small problem's few tiles (36 at B = 1024/view) spread over the chip.
-template <typename T>
+template <typename T, bool PERM = true>
 __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
   const int lane = threadIdx.x;
@@ -1260,7 +1272,7 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
         }
       }
     }
-  coef_epilogue<T, 1, 4>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
 }
 
 // ------------------------------------------------------------------------------------
