@@ -1,12 +1,20 @@
 #!/bin/bash
-# Same-box A/B of two native bench binaries (rocprof kernel averages, interleaved twice).
-# usage: tools/gpu_binab.sh BIN_A BIN_B [bench args...]
+# Same-call A/B of build/bin/ntxent_bench (working tree) vs build/bin/ntxent_bench_old
+# (tools/build_ab_old.sh REV), interleaved rounds; rocprofv3 kernel averages of the GEMMs.
+# usage: tools/gpu_binab.sh TAG [rounds]
 set -o pipefail
-A=$1; B=$2; shift 2
-OUT=$GRAFT_REPO_ROOT/gpurun_out/binab; mkdir -p $OUT
 export TMPDIR=/tmp
-for X in $A $B $A $B; do
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/$X -o run --output-format csv -- build/bin/$X --batch 4096 --dim 2048 --iters 20 --warmup 3 "$@" > $OUT/$X.log 2>&1 || exit 1
-  echo "$X $(tail -1 $OUT/$X.log | cut -c1-150)"
-  python tools/show_prof.py $OUT/$X/run_kernel_stats.csv 3
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-binab}; mkdir -p $OUT
+R=${2:-3}
+for rep in $(seq 1 $R); do
+for b in new old; do
+  BIN=build/bin/ntxent_bench; [ $b = old ] && BIN=build/bin/ntxent_bench_old
+  for c in "head --batch 4096 --dim 2048" "cfg2 --batch 4096 --dim 512" "cfg5 --batch 8192 --dim 1024 --compute fp16"; do
+    set -- $c; t=$1; shift
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/p_${t}_${b}_$rep -o run --output-format csv -- $BIN "$@" --iters 20 --warmup 5 > $OUT/${t}_${b}_$rep.log 2>&1 || { echo "$t $b failed"; exit 1; }
+    f=$(find $OUT/p_${t}_${b}_$rep -name '*kernel_stats.csv' | head -1)
+    echo "$t $b r$rep: fwdbwd=$(grep -A1 'fwd+bwd' $OUT/${t}_${b}_$rep.log | tail -1 | awk -F'|' '{print $4}' | awk '{print $1}') fwdgemm=$(grep -h 'Li0ELi0ELi1E' $f | cut -d, -f4) dz=$(grep -h 'Li2ELi0ELi1E' $f | cut -d, -f4)"
+  done
 done
+done
+echo done
