@@ -12,10 +12,13 @@ from ntxent_amd.ops import reference as R
 
 pytestmark = pytest.mark.gpu
 
-TOL = {  # (loss rtol, grad max-abs err relative to max |grad|)
-    "fp32": (2e-5, 2e-4),
-    "fp16": (3e-3, 2e-2),
-    "bf16": (1.5e-2, 6e-2),
+# (loss rtol, grad max-abs err relative to max |grad|): 2x the largest errors measured over the
+# shapes below on MI355X (profiles/r2/parity_kernels.log: fp32 8.5e-10 / 2.8e-6, fp16 6.0e-7 /
+# 3.9e-3, bf16 3.1e-7 / 1.1e-2; the kernels are deterministic, so box-to-box these do not move)
+TOL = {
+    "fp32": (2e-9, 6e-6),
+    "fp16": (1.2e-6, 8e-3),
+    "bf16": (7e-7, 2.2e-2),
 }
 
 
