@@ -1284,11 +1284,33 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.out_f16 = out_f16 ? 1 : 0;
   p.ldo = g.dim_n;
   p.slab_stride = (long long)g.rows_pad * g.dim_n;
-  const int grid = apply_schedule(p, ntiles, ws, stream);
+  // tile-starved (d <= 1024 at 8192 rows): split-K pieces + a parallel reduce instead of the
+  // stream-K schedule's serial last-arriver fixup (same rule as the forward's)
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  int pieces = fwd_splitk_pieces(ntiles, nk, cus, 1);
+  if (pieces < 3) pieces = 0;  // 2 pieces: the reduce launch costs more than the fixup it replaces
+  int grid;
+  if (pieces > 0) {
+    p.nk = nk;
+    p.dp_tiles = 0;
+    p.sk_tiles = ntiles;
+    p.ipb = (nk + pieces - 1) / pieces;
+    p.sk_out = 1;
+    p.sk_cnt = static_cast<int*>(ws.ptr);
+    p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+    grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
+    NTXENT_CHECK(p.kbytes % kKStepBytes == 0 && grid <= ws.num_cus && ws.ptr != nullptr &&
+                     ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
+                 "split-K dZ: workspace too small");
+  } else {
+    grid = apply_schedule(p, ntiles, ws, stream);
+  }
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
   });
+  if (pieces > 0) hipLaunchKernelGGL(dev::sk_dz_reduce_kernel, dim3(ntiles * 64), dim3(256), 0, stream, p);
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 

@@ -1588,5 +1588,54 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
   p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
 }
 
+// ------------------------------------------------------------------------------------
+// Split-K dZ for tile-starved dZ GEMMs (d <= 1024 at 8192 rows: 64 tiles x 128 K-steps on 256
+// CUs): the K pieces publish fp32 partial tiles (sk_out) and this launch sums each tile's
+// pieces in block order (deterministic) and writes the dZ tile exactly as the GEMM's epilogue
+// would (fp16 or fp32, optionally accumulated), 64 blocks per tile: block (w, k) = fragments
+// 4k..4k+3 of GEMM wave w, one (fragment, lane) per thread (one batch of slab loads in flight).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
+  const int tile = blockIdx.x >> 6, w = (blockIdx.x >> 3) & 7, kq = blockIdx.x & 7;
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y;
+  const int nk = p.nk;
+  const long long ipb = p.ipb;
+  const int b0 = (int)((long long)tile * nk / ipb), b1 = (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
+  auto slab = [&](int bb) {
+    const long long st = (long long)bb * ipb;
+    const bool first_partial = (st / nk == tile) && (st % nk != 0);
+    return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
+  };
+  const int wa = w >> 2, wb = w & 3;
+  {
+    const int u = threadIdx.x + 256 * kq, f = u >> 6, lane = u & 63;
+    const int off = ((w * 32 + f) * 64 + lane) * 4;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int bb = b0; bb <= b1; bb += 4) {  // 4 slab loads in flight (clamped, weighted)
+      f32x4 x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab(bb + q <= b1 ? bb + q : b1) + off));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v += x[q] * (bb + q <= b1 ? 1.f : 0.f);
+    }
+    const int mi = f >> 2, ni = f & 3;
+    const int rb = 128 * (mi >> 2) + 64 * wa + 16 * (mi & 3), cb = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
+    // swapped orientation (as the dZ epilogue): out[m = rb + (lane & 15)][n = cb + 4 (lane >> 4) + r]
+    const long long row = (long long)mt * kTile + rb + (lane & 15);
+    const int col = nt * kTile + cb + 4 * (lane >> 4);
+    if (p.out_f16) {
+      union { _Float16 h[4]; u32x2 u; } pk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)v[r];
+      *reinterpret_cast<u32x2*>(reinterpret_cast<_Float16*>(p.out) + row * p.ldo + col) = pk.u;
+    } else {
+      f32x4* o = reinterpret_cast<f32x4*>(p.out + row * p.ldo + col);
+      *o = p.accum ? *o + v : v;
+    }
+  }
+}
+
 }  // namespace dev
 }  // namespace ntxent

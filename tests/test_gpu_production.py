@@ -162,16 +162,20 @@ def test_diag_strips_match_stream_k(ext, rows, dim, T, compute):
 
 
 @pytest.mark.parametrize("rows,dim,T,compute", [(2048, 8192, 0.07, "fp16"), (2048, 4096, 0.02, "fp32"),
-                                                (1000, 6000, 0.07, "bf16")])
+                                                (1000, 6000, 0.07, "bf16"), (8192, 512, 0.07, "fp16"),
+                                                (8192, 256, 0.02, "fp32")])
 def test_splitk_reduce_matches_stream_k(ext, rows, dim, T, compute):
-    """Tile-starved forward (BASELINE config 4: 36 tiles x 128 K-steps on 256 CUs): the split-K
-    pieces + strip-parallel reduce (default) against the stream-K last-arriver fixup, and both
+    """Tile-starved GEMMs: the forward at BASELINE config 4 (36 tiles x 128 K-steps on 256 CUs)
+    and the dZ GEMM at config 2 (8192 rows, d = 512: 64 tiles x 128 K-steps) run as split-K
+    pieces + a parallel reduce (default); against the stream-K last-arriver fixup, and both
     against the fp64 oracle; fixed-shift and per-row-max epilogues, padded rows (1000)."""
-    nk = (dim + 63) // 64 * 64 * (4 if compute == "fp32" else 2) // 128
+    cs = 4 if compute == "fp32" else 2
+    cus = ext.device_info(0)["num_cus"]
     rt = (rows + 255) // 256
-    ntiles = rt * (rt + 1) // 2
+    fwd = ext.fwd_splitk_pieces(rt * (rt + 1) // 2, (dim + 63) // 64 * 64 * cs // 128, cus, rt)
+    dz = ext.fwd_splitk_pieces(rt * ((dim + 255) // 256), rt * 256 * cs // 128, cus, 1)
     assert ext.splitk_reduce_enabled()
-    assert ext.fwd_splitk_pieces(ntiles, nk, ext.device_info(0)["num_cus"], rt) >= 2
+    assert fwd >= 2 or dz >= 2
     dt = torch.float32 if compute == "fp32" else torch.bfloat16
     h = _views(rows, dim, seed=11 + dim, noise=2.0, dtype=dt)  # noisy views: O(1) loss
     l0, g0 = _run(h, T, compute)
