@@ -348,6 +348,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-small") o.small = false;
     else if (a == "--no-strips") ntxent::set_diag_strips(false);
     else if (a == "--no-splitk") ntxent::set_splitk_reduce(false);
+    else if (a == "--no-subtiles") ntxent::set_diag_subtiles(false);
     else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
     else if (a == "--exp") g_exp_backward = true;
     else if (a == "--no-exp") g_exp_backward = false;

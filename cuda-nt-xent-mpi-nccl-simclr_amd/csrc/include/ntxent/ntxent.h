@@ -194,6 +194,8 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
 // main_done (optional): recorded on `stream` right after the persistent GEMM, before the strips.
 // Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
 void set_diag_strips(bool on);
+// Diagonal remainder as 64x64 sub-tiles (default) or 16-row strips (off, for A/B).
+void set_diag_subtiles(bool on);
 bool diag_strips_enabled();
 // Split-K forward for own-block launches with fewer tiles than CUs and long K (on by default;
 // off = the stream-K schedule's serial last-arriver fixup, for A/B): K pieces of every tile

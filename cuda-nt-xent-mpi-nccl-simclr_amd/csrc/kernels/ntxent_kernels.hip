@@ -1088,6 +1088,8 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
+static std::atomic<bool> g_diag_sub{true};
+void set_diag_subtiles(bool on) { g_diag_sub = on; }
 static std::atomic<bool> g_diag_strips{true};
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1178,7 +1180,13 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         if (q.sc) q.sc += (size_t)nmain * kTileElems * sizeof(typename dev::StoreT<Tc>::type);
         const dim3 sg(nstrip * 16);
         const bool one_wave = nstrip * 16 <= ws.num_cus;  // 3-stage ring, else 2 blocks per CU
-        if (p.fixed_shift) {
+        if (g_diag_sub.load() && 4 * nstrip <= 2 * ws.num_cus) {  // 64x64 sub-tiles (row-group tickets)
+          q.sk_cnt = static_cast<int*>(ws.ptr);
+          float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
+                                                      (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
+          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
+          else hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
+        } else if (p.fixed_shift) {
           if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 3>), sg, dim3(256), 0, stream, q);
           else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q);
         } else {

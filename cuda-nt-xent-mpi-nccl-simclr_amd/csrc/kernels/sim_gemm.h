@@ -1434,6 +1434,156 @@ __global__ __launch_bounds__(256) void diag_strip_kernel(const SimParams p) {
 }
 
 // ------------------------------------------------------------------------------------
+// Diagonal tiles as 64x64 sub-tiles (the forward's whole-round remainder, alternative to the
+// 16-row strips): 16 blocks per tile, block (a, b) computes S[64a.., 64b..] with a 3-stage LDS
+// ring shared by its 4 waves (64 A + 64 B rows per K-step, one barrier per step), wave w rows
+// 64a + 16w.. x all 64 columns. A block reads 128 rows per K-step instead of a strip block's
+// 4 x 80, so the L2 -> CU traffic is 2.5x smaller. Row partials over the sub-tile's 64 columns
+// go to write-through scratch rows[tile][a][b][64]; the 4th block of a row group (ticket) merges
+// them in b order (deterministic). Masks, partial forms and kept cosines as the GEMM epilogue.
+// ------------------------------------------------------------------------------------
+// 3 stages (49 KiB: 3 blocks per CU fit, which the 512 sub-tiles of config 5 need); a 6-stage
+// ring (5 K-steps in flight) measured the same at the headline (profiles/r2/subtiles): the loop
+// is bound by the per-step LDS-DMA issue and barrier, not by load latency.
+constexpr int kSubStage = 128 * kKStepBytes;   // 64 A + 64 B rows = 16 KiB
+constexpr int kSubStages = 3;
+constexpr int kSubLds = kSubStages * kSubStage + 1024;  // + the ticket flag
+template <typename T, int FX>
+__global__ __launch_bounds__(256) void diag_sub_kernel(const SimParams p, float2* __restrict__ scratch) {
+  using MM = Mfma<T>;
+  typedef typename MM::frag frag;
+  typedef typename StoreT<T>::type TS;
+  typedef __attribute__((address_space(3))) const frag lds_frag;
+  __shared__ __attribute__((aligned(16))) char smem[kSubLds];  // one array (see diag_strip_body)
+  lds_char* lds = (lds_char*)smem;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 sub-tiles share one XCD
+  const int tile = idx >> 4, a = (idx >> 2) & 3, b = idx & 3;
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y;
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  // DMA piece j of wave w: ring rows 32w + 8j + (lane >> 3) (rows 0-63 A = tile rows 64a..,
+  // 64-127 B = tile columns 64b..), 16-byte chunk (lane & 7) ^ ((row >> 1) & 7)
+  const char* src[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = 32 * w + 8 * j + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    src[j] = row < 64 ? p.A.base + (long long)mt * p.A.row_tile_stride + (long long)(64 * a + row) * p.A.ld + 16 * chunk
+                      : p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride +
+                            (long long)(64 * b + row - 64) * p.B.ld + 16 * chunk;
+  }
+  auto stage = [&](int s, int buf) {
+    const long long o = (long long)s * kKStepBytes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src[j] + o),
+                                       (lds_void*)(lds + buf * kSubStage + (32 * w + 8 * j) * kKStepBytes), 16, 0, 0);
+  };
+  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
+  f32x4 acc[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int P = kSubStages - 1;  // K-steps in flight
+#pragma unroll
+  for (int i = 0; i < P; ++i) stage(i < nk ? i : nk - 1, i);
+  int buf = 0;
+  for (int s = 0; s < nk; ++s) {
+    // own pieces of step s landed (the P - 1 younger steps' 4 each in flight); after the
+    // barrier every wave's have, and every wave has finished reading the buffer refilled next
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    static_assert(4 * (P - 1) == 4, "vmcnt count = pieces per step x (P - 1)");
+    __builtin_amdgcn_s_barrier();
+    const int nb2 = buf == 0 ? kSubStages - 1 : buf - 1;  // (s + P) % kSubStages
+    stage(s + P < nk ? s + P : nk - 1, nb2);
+    const lds_char* st = lds + buf * kSubStage;
+    frag af[2], bf[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int pch = ((4 * c + cq) ^ sw) << 4;
+      af[c] = *(lds_frag*)(st + (16 * w + r16) * kKStepBytes + pch);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) bf[c][f] = *(lds_frag*)(st + (64 + 16 * f + r16) * kKStepBytes + pch);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] = MM::mma(af[c], bf[c][f], acc[f]);
+    buf = buf == kSubStages - 1 ? 0 : buf + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
+  // lane holds S[row 64a + 16w + 4 (lane >> 4) + r][col 64b + 16 f + (lane & 15)] (tile-local)
+  const int rb0 = 64 * a + 16 * w;
+  if (p.sc) {  // kept cosines, canonical fragment order, before the masks
+    TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
+    const float cs = p.cos_scale;
+    if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+      for (int np = 0; np < 2; ++np) {
+        union { TS h[8]; u32x4 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pk.h[r] = from_f32<TS>(acc[2 * np][r] * cs);
+          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r] * cs);
+        }
+        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * np, lane) * 8) = pk.u;
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * b + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f] * cs;
+    }
+  }
+  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
+  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+  const float sc_ = p.acc_scale, M = p.y_scale;
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + a) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tr = rb0 + 4 * (lane >> 4) + r, gi = r0 + tr;
+    float y[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int tc = 64 * b + 16 * f + (lane & 15), d = tc - tr;
+      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
+                        ((d == D2) & (gi >= p.n_half));
+      y[f] = drop ? kNegInf : acc[f][r] * sc_;
+    }
+    float m = M;
+    if constexpr (!FX) m = row16_max(fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
+    const float ms = (m == kNegInf) ? 0.f : m;
+    float sr = (fast_exp2(y[0] - ms) + fast_exp2(y[1] - ms)) + (fast_exp2(y[2] - ms) + fast_exp2(y[3] - ms));
+    sr = row16_sum(sr);
+    const float mo = FX ? (sr > 0.f ? M : kNegInf) : m;
+    if ((lane & 15) == 0)  // write-through: merged by the row group's last block on any XCD
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mo), __float_as_uint(sr)}, srs,
+                                            (b * 64 + 16 * w + 4 * (lane >> 4) + r) * 8, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem + kSubStages * kSubStage);
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(p.sk_cnt + tile * 4 + a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == 3;
+    if (last) __hip_atomic_store(p.sk_cnt + tile * 4 + a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0] || threadIdx.x >= 64) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  const int i = threadIdx.x;
+  u32x2 q[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b64(srs, (k * 64 + i) * 8, 0, 16);
+  float m = __uint_as_float(q[0][0]), s = __uint_as_float(q[0][1]);
+#pragma unroll
+  for (int k = 1; k < 4; ++k) lse_merge(m, s, __uint_as_float(q[k][0]), __uint_as_float(q[k][1]));
+  p.part[(long long)nt * p.Rpad + r0 + 64 * a + i] = make_float2(m, s);
+}
+
+// ------------------------------------------------------------------------------------
 // Split-K forward for tile-starved launches (fewer tiles than CUs, long K: BASELINE config 4,
 // 36 tiles x 128 K-steps): every K piece of the persistent GEMM publishes its fp32 partial tile
 // (sk_out), and this launch sums each tile's pieces (fixed block order: deterministic) and runs

@@ -841,6 +841,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_exp_backward", &set_exp_backward, py::arg("on"));
   m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
   m.def("set_splitk_reduce", &ntxent::set_splitk_reduce, py::arg("on"));
+  m.def("set_diag_subtiles", &ntxent::set_diag_subtiles, py::arg("on"));
   m.def("splitk_reduce_enabled", &ntxent::splitk_reduce_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
