@@ -360,7 +360,10 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
 }
 
 // 64x64 tile transpose with 16-byte global accesses on both sides (rows of Zq in, rows of
-// ZqT out); the LDS tile is padded by 16 B per row.
+// ZqT out). LDS: 16-byte chunk c of row r sits at chunk c ^ ((r / V) % CPR), so the column
+// gathers (V rows r = V jc + q of one column per lane group) hit distinct banks (the padded
+// linear layout alone left them 4-way conflicted: 3.7M SQ_LDS_BANK_CONFLICT per launch at the
+// headline, profiles/r2/pmc_final).
 template <typename T>
 __device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __restrict__ zqt, int dk, int ldk, int ldt,
                                                int bx, int by, T (&tile)[64][64 + 16 / sizeof(T)]) {
@@ -371,14 +374,14 @@ __device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __re
     const int r = k / CPR, c = k % CPR;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * ldk + e0 + c * V);
-    *reinterpret_cast<u32x4*>(&tile[r][c * V]) = v;
+    *reinterpret_cast<u32x4*>(&tile[r][(c ^ ((r / V) % CPR)) * V]) = v;
   }
   __syncthreads();
   for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
     const int er = k / CPR, jc = k % CPR;
     union { T h[V]; u32x4 u; } pk;
 #pragma unroll
-    for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][er];
+    for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][((er / V) ^ (jc % CPR)) * V + er % V];
     *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
   }
 }
