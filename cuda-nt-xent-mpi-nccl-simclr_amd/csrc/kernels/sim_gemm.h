@@ -1007,6 +1007,32 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] *= p.out_scale;
     }
     float* out = p.out;
+    if (!kDzE && p.out_f16 && !p.accum) {
+      // fp16 tile through LDS (free after the main loop): fragments -> row-major [256][256] with
+      // the 16-byte chunk index XORed by (row & 15) (conflict-free both ways), then 512-byte
+      // coalesced rows out. A fragment's direct 8-byte stores put 16 rows in every instruction.
+      typedef __attribute__((address_space(3))) u32x2 lds_u2;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const int rt = rb[mi] + (lane & 15);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int ct = cb[ni] + 4 * (lane >> 4);
+          union { _Float16 h[4]; u32x2 u; } pk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
+          *(lds_u2*)(lds + rt * 512 + ((((ct >> 3) ^ (rt & 15))) << 4) + ((ct >> 2) & 1) * 8) = pk.u;
+        }
+      }
+      __syncthreads();
+      _Float16* o16 = reinterpret_cast<_Float16*>(out) + ((long long)mt * kTile) * p.ldo + nt * kTile;
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
+        const u32x4 v = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
+        *reinterpret_cast<u32x4*>(o16 + (long long)rt * p.ldo + c * 8) = v;
+      }
+    } else {
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const long long row = (long long)mt * kTile + rb[mi] + (lane & 15);
@@ -1023,6 +1049,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
         }
       }
+    }
     }
   } else if constexpr (MODE == kModeCoef) {
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
