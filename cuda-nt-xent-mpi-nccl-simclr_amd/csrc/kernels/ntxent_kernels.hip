@@ -1183,7 +1183,11 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         if (q.sc) q.sc += (size_t)nmain * kTileElems * sizeof(typename dev::StoreT<Tc>::type);
         const dim3 sg(nstrip * 16);
         const bool one_wave = nstrip * 16 <= ws.num_cus;  // 3-stage ring, else 2 blocks per CU
-        if (g_diag_sub.load() && 4 * nstrip <= 2 * ws.num_cus) {  // 64x64 sub-tiles (row-group tickets)
+        // 64x64 sub-tiles (row-group tickets) unless K is short and the strips fit in one wave of
+        // blocks (config 2, d = 512: strips 7.4 vs sub-tiles 8.0 us; headline 17.0 vs 15.3,
+        // config 5 18.5 vs 12.9: profiles/r2/subtiles)
+        const bool sub = (p.kbytes / kKStepBytes) >= 16 || !one_wave;
+        if (g_diag_sub.load() && sub && 4 * nstrip <= 2 * ws.num_cus) {
           q.sk_cnt = static_cast<int*>(ws.ptr);
           float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                       (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
