@@ -302,13 +302,14 @@ def run_rank(a) -> None:
         step()
     if on_gpu:
         torch.cuda.reset_peak_memory_stats(dev)
-    # The timed region has no per-step events (a timing event recorded between two steps left a
-    # ~5-8 us bubble per step in the kernel trace); the per-step distribution comes from a
-    # separate pass right after it.
-    dt_s, _, comm_ms, loss, gh = timed(step, a.steps, a.warmup, per_step_events=False, comm=world > 1)
-    per_ms = None
-    if on_gpu:
-        _, per_ms, _, _, _ = timed(step, min(a.steps, 20), 0, per_step_events=True)
+    # The timed region records no events at all, at every N (a timing event recorded between two
+    # steps left a ~5-8 us bubble per step in the kernel trace, and the communication spans would
+    # add several per step at N > 1): the per-step distribution and the per-rank communication
+    # waits come from a separate pass right after it.
+    dt_s, _, _, loss, gh = timed(step, a.steps, a.warmup, per_step_events=False, comm=False)
+    per_ms = comm_ms = None
+    if on_gpu or world > 1:
+        _, per_ms, comm_ms, _, _ = timed(step, min(a.steps, 20), 0, per_step_events=on_gpu, comm=world > 1)
     peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20 if on_gpu else None
     lossv = float(loss.item())
     finite = bool(lossv == lossv and torch.isfinite(gh).all().item())

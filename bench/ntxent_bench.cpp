@@ -139,7 +139,6 @@ void* upload(std::vector<float>& host, DType in) {
   return d;
 }
 
-bool g_exp_backward = false;  // --exp: the coefficient-free backward (A/B against the coefficient pass)
 
 class Bench {
  public:
@@ -155,7 +154,6 @@ class Bench {
     c.keep_cos = keep_cos;
     c.small_path = small_path;
     c.small_splits = small_splits;
-    c.exp_backward = g_exp_backward;
     host_ = synthetic_views(c.rows, dim, seed);
     h_ = upload(host_, in);
     NTXENT_HIP_CHECK(hipMalloc(&dh_, host_.size() * dtype_size(in)));
@@ -350,8 +348,6 @@ int main(int argc, char** argv) {
     else if (a == "--no-splitk") ntxent::set_splitk_reduce(false);
     else if (a == "--no-subtiles") ntxent::set_diag_subtiles(false);
     else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
-    else if (a == "--exp") g_exp_backward = true;
-    else if (a == "--no-exp") g_exp_backward = false;
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"

@@ -40,9 +40,6 @@ struct EngineConfig {
   DType compute = DType::F16;
 #endif
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
-  // eligible plans (exp_backward_eligible) keep exponentials instead and run the
-  // coefficient-free backward (launch_dz_exp): no coefficient pass, no coefficient buffer
-  bool exp_backward = false;  // (off by default until its dZ GEMM beats coefficient pass + dZ)
   bool check_finite = false;  // loss() throws on a non-finite loss
   bool small_path = true;     // single-rank small problems: the one-launch fwd / bwd kernels
   int small_splits = 0;       // small path: backward column splits (0: small_bwd_splits)
@@ -98,7 +95,6 @@ class Engine {
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
   bool small_ = false;        // small-problem path (small_kernels.hip)
-  bool exp_ = false;          // coefficient-free backward (sbuf_ holds the exponential store)
   void* small_scratch_ = nullptr;
   DType bwd_ = DType::F16;
   void* arena_ = nullptr;

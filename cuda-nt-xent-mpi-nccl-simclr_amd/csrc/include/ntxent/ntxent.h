@@ -178,9 +178,6 @@ struct BlockView {
 // part_x (symmetric mode, kTileCross tiles): column partials for the partner's rows,
 // part_x[(q * row_tiles + mt) * Rpad + (nt % row_tiles) * 256 + c] with q = nt / row_tiles,
 // i.e. rank q's part slots [rank*row_tiles + mt] for its rows.
-// store_exp (exp_backward_eligible plans, all-gather layout): keep E = 2^(y - M) (bf16) in
-// `sc` instead of the cosines, exp_store_elems(g) elements in exp_slot order (own-block upper
-// triangle, then the remote tiles), masked elements (self, positive, padding) exactly 0.
 // diag_tail: the last `diag_tail` entries of `tiles` are kTileDiag tiles (own_diag_tail(g) for
 // a launch that ends with the own block, else 0). When the persistent GEMM's tile count leaves a
 // remainder of at most that many tiles after its whole rounds, the remainder runs as 16-row
@@ -189,7 +186,7 @@ struct BlockView {
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                      const BlockView& bv = BlockView{}, float2* part_x = nullptr, bool store_exp = false,
+                      const BlockView& bv = BlockView{}, float2* part_x = nullptr,
                       int diag_tail = 0, hipEvent_t main_done = nullptr);
 // main_done (optional): recorded on `stream` right after the persistent GEMM, before the strips.
 // Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
@@ -206,20 +203,18 @@ void set_coef_lane_permute(bool on);
 bool coef_lane_permute();
 void set_splitk_reduce(bool on);
 bool splitk_reduce_enabled();
+// Small-problem path (on by default; off = the large-problem pipeline for every shape) and its
+// backward column splits (0 = small_bwd_splits).
+void set_small_path(bool on);
+bool small_path_enabled();
+void set_small_splits(int n);
+int small_splits_override();
+// CUs the similarity GEMMs launched while it is non-zero leave free for communication kernels
+// (the data-parallel paths set it around launches that overlap an RCCL transfer); returns the
+// old value.
+int set_grid_reserve(int n);
+int grid_reserve();
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
-
-// ---- coefficient-free backward ---------------------------------------------------------------
-// Plans whose forward can keep exponentials for it: reduced precision, fixed-shift epilogue
-// (tau > ~0.024) and W * Rpad <= 8192 (the dZ GEMM holds a table of every row's a_i in LDS).
-bool exp_backward_eligible(const Geometry& g, DType comp);
-size_t exp_store_elems(const Geometry& g);  // bf16 elements of the exponential tile store
-int exp_coef_shift(const Geometry& g);      // s: C is formed as 2^s * C in the MFMA dtype
-// dZ = C' * Z from the exponential store `ebuf` (launch_fwd_stats store_exp) and the gathered
-// lse2: C'_ij = E_ij (a_i + a_j) = P_ij + P_ji, formed per K-step in LDS (no coefficient buffer).
-// The positive pair is NOT included (its E is 0): launch_norm_bwd adds cpos_i * zq_p(i) (PosTerm).
-void launch_dz_exp(DType comp, const void* ebuf, const void* zqt_all, const float* lse2_all, const int4* tiles,
-                   int ntiles, void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                   bool out_f16 = false);
 
 // Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
@@ -273,18 +268,9 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 // xslabs (optional): nx more fp16 slabs [nx][Rpad][dim_n] added to the sum (received partner
 // contributions of the symmetric data-parallel mode, or the fp16 dZ of a reduced-precision plan
 // and nslabs = 0 fp32 slabs).
-// pos (exponential backward): also add cpos[i] * zq[p(i)] to row i's gradient (zq in the
-// backward dtype, rows `ld` elements apart).
-struct PosTerm {
-  const void* zq = nullptr;
-  DType zdt = DType::F16;
-  int ld = 0;
-  const float* cpos = nullptr;
-};
 void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h,
                      const float* inv, const float* grad_out, void* dh, const Geometry& g,
-                     hipStream_t stream, const void* xslabs = nullptr, int nx = 0,
-                     const PosTerm& pos = PosTerm{});
+                     hipStream_t stream, const void* xslabs = nullptr, int nx = 0);
 
 // ---- small-problem path (kernels/small_kernels.hip) -------------------------------------
 // Single-rank problems with R <= kSmallMaxRows and dim_k <= kSmallMaxDk in fp16/bf16: after

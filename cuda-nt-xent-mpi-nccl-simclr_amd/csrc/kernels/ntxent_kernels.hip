@@ -524,25 +524,14 @@ __global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int
 // Vectorised normalisation backward: one 256-thread block per row; each thread owns NCH
 // chunks of 8 contiguous features, kept in registers between the dot pass and the output.
 // xs: nx extra fp16 slabs (received partner contributions, symmetric data-parallel mode) added
-// to the fp32 sum. zdt != 0 (exponential backward, whose dZ GEMM leaves the positive pair out):
-// g += cpos[i] * zq[p(i)], zq rows zld elements apart in fp16 (zdt 1) or bf16 (zdt 2).
-struct PosArgs {
-  const void* zq;
-  const float* cpos;
-  int zld, zdt, n_half;
-};
-__device__ __forceinline__ void pos_load8(const PosArgs& pa, int i, int e, float (&v)[8]) {
-  const long long ip = i < pa.n_half ? i + pa.n_half : i - pa.n_half;
-  if (pa.zdt == 1) load8<_Float16>(static_cast<const _Float16*>(pa.zq) + ip * pa.zld + e, v);
-  else load8<__bf16>(static_cast<const __bf16*>(pa.zq) + ip * pa.zld + e, v);
-}
+// to the fp32 sum.
 template <typename Tin, int NCH>
 __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restrict__ slabs, int nslabs,
                                                            long long slab_stride, long long ldo,
                                                            const Tin* __restrict__ h, const float* __restrict__ inv,
                                                            const float* __restrict__ grad_out, float alpha_base,
                                                            Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
-                                                           int nx, const PosArgs pa) {
+                                                           int nx) {
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -572,13 +561,6 @@ __global__ __launch_bounds__(256) void norm_bwd_vec_kernel(const float* __restri
       }
       g[c][0] = a[0]; g[c][1] = a[1]; g[c][2] = a[2]; g[c][3] = a[3];
       g[c][4] = b[0]; g[c][5] = b[1]; g[c][6] = b[2]; g[c][7] = b[3];
-      if (pa.zdt != 0) {
-        float zp[8];
-        pos_load8(pa, i, e, zp);
-        const float cp = pa.cpos[i];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[c][j] += cp * zp[j];
-      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) { z[c][j] *= iv; dot += z[c][j] * g[c][j]; }
     }
@@ -604,15 +586,8 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
                                                        const Tin* __restrict__ h, const float* __restrict__ inv,
                                                        const float* __restrict__ grad_out, float alpha_base,
                                                        Tin* __restrict__ dh, int d, const _Float16* __restrict__ xs,
-                                                       int nx, const PosArgs pa) {
+                                                       int nx) {
   const _Float16* xi = xs + (long long)blockIdx.x * ldo;
-  const long long ip = blockIdx.x < pa.n_half ? blockIdx.x + pa.n_half : (long long)blockIdx.x - pa.n_half;
-  const float cp = pa.zdt != 0 ? pa.cpos[blockIdx.x] : 0.f;
-  auto zpos = [&](int e) -> float {
-    if (pa.zdt == 0) return 0.f;
-    return pa.zdt == 1 ? (float)static_cast<const _Float16*>(pa.zq)[ip * pa.zld + e]
-                       : (float)static_cast<const __bf16*>(pa.zq)[ip * pa.zld + e];
-  };
   __shared__ float red[16];
   const int i = blockIdx.x;
   const float iv = inv[i];
@@ -624,7 +599,6 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
     float g = 0.f;
     for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
-    g += cp * zpos(e);
     dot += to_f32<Tin>(hi[e]) * iv * g;
   }
   dot = block_sum(dot, red);
@@ -633,7 +607,6 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
     float g = 0.f;
     for (int k = 0; k < nslabs; ++k) g += gi[k * slab_stride + e];
     for (int k = 0; k < nx; ++k) g += (float)xi[k * slab_stride + e];
-    g += cp * zpos(e);
     const float z = to_f32<Tin>(hi[e]) * iv;
     di[e] = from_f32<Tin>(alpha * iv * (g - z * dot));
   }
@@ -673,130 +646,10 @@ void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
   p.scale_off = comp == DType::FP8 ? g.dim_k8 : 0;
 }
 
-// Diagnostic builds (-DNTXENT_ABLATION_KERNELS) pick a compile-time ablation of the GEMM
-// main loop with NTXENT_GEMM_ABL=<bits>; production builds instantiate only ABL = 0.
-int gemm_ablation() {
-#ifdef NTXENT_ABLATION_KERNELS
-  static const int a = [] {
-    const char* e = std::getenv("NTXENT_GEMM_ABL");
-    return e ? std::atoi(e) : 0;
-  }();
-  return a;
-#else
-  return 0;
-#endif
-}
-
 template <typename Tc, int MODE>
 void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
-#ifdef NTXENT_ABLATION_KERNELS
-  if constexpr (MODE == dev::kModeDzE && std::is_same<Tc, _Float16>::value) switch (gemm_ablation()) {
-    // coefficient-free dZ: 1 no DMA, 2 no A reads, 4 no MFMA, 128 no transform, 64 timeline
-#define NTXENT_ABL_E(A) \
-    case A: hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); return;
-    NTXENT_ABL_E(1) NTXENT_ABL_E(2) NTXENT_ABL_E(4) NTXENT_ABL_E(128) NTXENT_ABL_E(129) NTXENT_ABL_E(130)
-    NTXENT_ABL_E(6) NTXENT_ABL_E(134) NTXENT_ABL_E(256) NTXENT_ABL_E(512) NTXENT_ABL_E(258) NTXENT_ABL_E(514) NTXENT_ABL_E(1152) NTXENT_ABL_E(2176)
-#undef NTXENT_ABL_E
-    default: break;
-  }
-  if constexpr (std::is_same<Tc, _Float16>::value || std::is_same<Tc, dev::fp8e4m3>::value) switch (gemm_ablation()) {
-    // fp8: only the timeline build (64) is instantiated
-#define NTXENT_ABL_CASE(A) \
-    case A:                                                                                                  \
-      if constexpr ((std::is_same<Tc, _Float16>::value && MODE != dev::kModeDzE) || (A == 1 && std::is_same<Tc, dev::fp8e4m3>::value)) { \
-        hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, A>), dim3(grid), dim3(kGemmThreads), 0, stream, p); \
-        return;                                                                                              \
-      }                                                                                                      \
-      break;
-    NTXENT_ABL_CASE(1) NTXENT_ABL_CASE(2) NTXENT_ABL_CASE(3) NTXENT_ABL_CASE(4) NTXENT_ABL_CASE(5)
-    NTXENT_ABL_CASE(6) NTXENT_ABL_CASE(14) NTXENT_ABL_CASE(22) NTXENT_ABL_CASE(30)
-#undef NTXENT_ABL_CASE
-    case 32: {  // clock stamps of block 0 (waves 0 and 4), dumped to stderr (synchronising)
-
-      static unsigned long long* buf = nullptr;
-      if (!buf) NTXENT_HIP_CHECK(hipMalloc(&buf, 512 * 8));
-      NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, 512 * 8, stream));
-      dev::SimParams q = p;
-      q.stamps = buf;
-      hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 32>), dim3(grid), dim3(kGemmThreads), 0, stream, q);
-      unsigned long long h[512];
-      NTXENT_HIP_CHECK(hipMemcpyAsync(h, buf, sizeof(h), hipMemcpyDeviceToHost, stream));
-      NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
-      std::fprintf(stderr, "STAMPS mode=%d nk=%d", MODE, p.nk);
-      for (int g = 0; g < 2; ++g) {
-        std::fprintf(stderr, " | g%d:", g);
-        for (int i = 1; i < 256 && h[g * 256 + i]; ++i) std::fprintf(stderr, " %llu", h[g * 256 + i] - h[g * 256 + i - 1]);
-      }
-      std::fprintf(stderr, "\n");
-      return;
-    }
-    case 64: {  // per-block item timeline of every block, summarised to stderr (synchronising)
-      static unsigned long long* buf = nullptr;
-      static int cap = 0;
-      if (cap < grid) {
-        if (buf) NTXENT_HIP_CHECK(hipFree(buf));
-        NTXENT_HIP_CHECK(hipMalloc(&buf, (size_t)grid * 64 * 8));
-        cap = grid;
-      }
-      NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, (size_t)grid * 64 * 8, stream));
-      dev::SimParams q = p;
-      q.stamps = buf;
-      hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 64>), dim3(grid), dim3(kGemmThreads), 0, stream, q);
-      std::vector<unsigned long long> h((size_t)grid * 64);
-      NTXENT_HIP_CHECK(hipMemcpyAsync(h.data(), buf, h.size() * 8, hipMemcpyDeviceToHost, stream));
-      NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
-      unsigned long long t0 = ~0ull, t1 = 0;
-      double clk = 0, loop_full = 0, n_full = 0, loop_part = 0, steps_part = 0, pro = 0, fix = 0, epi = 0, tail = 0;
-      double n_items = 0, n_fix = 0, busy_max = 0, start_max = 0;
-      double ep[5] = {0, 0, 0, 0, 0};  // fwd epilogue phases: store, masks, exp+reduce, barrier, merge
-      for (int b = 0; b < grid; ++b) {
-        const unsigned long long* s = h.data() + (size_t)b * 64;
-        t0 = std::min(t0, s[0]);
-        t1 = std::max(t1, s[2]);
-        clk += (double)(s[2] - s[0]) / (double)std::max(1ull, s[3] - s[1]) * 0.1;  // GHz (100 MHz ref)
-      }
-      for (int b = 0; b < grid; ++b) {
-        const unsigned long long* s = h.data() + (size_t)b * 64;
-        start_max = std::max(start_max, (double)(s[0] - t0));
-        busy_max = std::max(busy_max, (double)(s[2] - s[0]));
-        tail += (double)(t1 - s[2]);
-        for (int k = 0; k < 9 && s[6 + 6 * k]; ++k) {
-          const unsigned long long* it = s + 4 + 6 * k;
-          const double loop = (double)(it[3] - it[2]);
-          if ((int)it[1] == p.nk) { loop_full += loop; n_full += 1; }
-          else { loop_part += loop; steps_part += (double)it[1]; }
-          fix += (double)(it[4] - it[3]);
-          n_fix += (int)it[1] != p.nk;
-          if (it[5]) epi += (double)(it[5] - it[4]);
-          if (it[5] && k < 6 && s[40 + 4 * k]) {
-            const unsigned long long* e = s + 40 + 4 * k;
-            ep[0] += (double)(e[0] - it[4]); ep[1] += (double)(e[1] - e[0]); ep[2] += (double)(e[2] - e[1]);
-            ep[3] += (double)(e[3] - e[2]); ep[4] += (double)(it[5] - e[3]);
-          }
-          n_items += 1;
-          // gap between the previous item's end and this one's start (loop bookkeeping)
-          pro += (double)(it[2] - (k == 0 ? s[0] : s[4 + 6 * (k - 1) + 5] ? s[4 + 6 * (k - 1) + 5] : s[4 + 6 * (k - 1) + 4]));
-        }
-      }
-      clk /= grid;
-      const double us = 1e-3 / clk;  // microseconds per cycle
-      std::fprintf(stderr,
-                   "TIMELINE mode=%d grid=%d nk=%d dp=%d sk=%d ipb=%lld clk=%.3fGHz span=%.1fus start_skew=%.1fus "
-                   "busy_max=%.1fus | per block: items=%.2f loop_full=%.1fus (%.0f cyc/kstep, %d tiles) "
-                   "loop_part=%.1fus (%.0f cyc/kstep) fixup=%.1fus epilogue=%.1fus [store %.1f masks %.1f exp %.1f "
-                   "bar %.1f merge %.1f] gaps=%.1fus tail_idle=%.1fus\n",
-                   MODE, grid, p.nk, p.dp_tiles, p.sk_tiles, p.ipb, clk, (t1 - t0) * us, start_max * us, busy_max * us,
-                   n_items / grid, loop_full / grid * us, n_full ? loop_full / n_full / p.nk : 0.0, (int)n_full,
-                   loop_part / grid * us, steps_part ? loop_part / steps_part : 0.0, fix / grid * us, epi / grid * us,
-                   ep[0] / grid * us, ep[1] / grid * us, ep[2] / grid * us, ep[3] / grid * us, ep[4] / grid * us,
-                   pro / grid * us, tail / grid * us);
-      return;
-    }
-    default: break;
-  }
-#endif
   if (MODE == dev::kModeFwd && !p.fixed_shift)
-    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, 0, MODE == dev::kModeFwd ? 0 : 1>), dim3(grid), dim3(kGemmThreads), 0,
+    hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, MODE == dev::kModeFwd ? 0 : 1>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
   else
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
@@ -817,15 +670,6 @@ dev::SimParams base_params(const Geometry& g) {
   p.acc_scale = p.y_scale;
   p.cos_scale = 1.0f;
   p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
-#ifdef NTXENT_ABLATION_KERNELS
-  static const int dbg = [] {  // runtime epilogue/load ablations (diagnostic builds only)
-    const char* e = std::getenv("NTXENT_GEMM_DEBUG");
-    return e ? std::atoi(e) : 0;
-  }();
-  p.dbg = dbg;
-#else
-  p.dbg = 0;
-#endif
   return p;
 }
 
@@ -992,9 +836,6 @@ GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
     const double cost = (double)nk / c + (c > 1 ? 10.0 + 4.0 * (c - 1) : 0.0);
     if (cost < best - 1e-9) { best = cost; p = c; }
   }
-#ifdef NTXENT_ABLATION_KERNELS
-  if (const char* e = std::getenv("NTXENT_SK_SPLIT")) p = std::max(1, std::min({std::atoi(e), G0 / rem, nk}));  // diagnostic builds only
-#endif
   s.grid = q > 0 ? G0 : rem * p;
   s.ipb = (nk + p - 1) / p;  // K-steps per stream-K block; ceil(rem * nk / ipb) <= rem * p blocks busy
   return s;
@@ -1091,17 +932,28 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-static std::atomic<bool> g_diag_sub{true};
+// ---- runtime switches: every process-wide toggle of the library lives here (atomics; the
+//      defaults are the measured-fastest choices, the setters exist for A/B tests) ----------
+static std::atomic<bool> g_diag_sub{true};       // diagonal remainder as 64x64 sub-tiles (else strips)
+static std::atomic<bool> g_diag_strips{true};    // forward remainder after whole rounds as strips/sub-tiles
+static std::atomic<bool> g_coef_perm{true};      // coefficient pass: lane-permuted row-major stores
+static std::atomic<bool> g_splitk_reduce{true};  // split-K forward / dZ for tile-starved launches
+static std::atomic<bool> g_small_path{true};     // one-launch small-problem forward / backward
+static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
+static std::atomic<int> g_grid_reserve{0};       // CUs the GEMMs leave free for overlapped RCCL kernels
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
-static std::atomic<bool> g_diag_strips{true};
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
-static std::atomic<bool> g_coef_perm{true};
 void set_coef_lane_permute(bool on) { g_coef_perm = on; }
 bool coef_lane_permute() { return g_coef_perm.load(); }
-static std::atomic<bool> g_splitk_reduce{true};
 void set_splitk_reduce(bool on) { g_splitk_reduce = on; }
 bool splitk_reduce_enabled() { return g_splitk_reduce.load(); }
+void set_small_path(bool on) { g_small_path = on; }
+bool small_path_enabled() { return g_small_path.load(); }
+void set_small_splits(int n) { g_small_splits = std::max(0, n); }
+int small_splits_override() { return g_small_splits.load(); }
+int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
+int grid_reserve() { return g_grid_reserve.load(); }
 
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
@@ -1114,7 +966,7 @@ int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
 
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
-                      hipStream_t stream, const BlockView& bv, float2* part_x, bool store_exp, int diag_tail,
+                      hipStream_t stream, const BlockView& bv, float2* part_x, int diag_tail,
                       hipEvent_t main_done) {
   if (ntiles == 0) return;
   NTXENT_CHECK(diag_tail >= 0 && diag_tail <= ntiles, "fwd_stats: bad diagonal tail");
@@ -1131,23 +983,18 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.sc = static_cast<char*>(sc);
   p.b_tile0 = bv.b_tile0;
   p.part_x = part_x;
-  if (store_exp) {
-    NTXENT_CHECK(exp_backward_eligible(g, comp) && sc != nullptr && bv.b_tile0 == 0 && part_x == nullptr,
-                 "fwd_stats: exponential store needs an exp-backward plan (see exp_backward_eligible)");
-    p.store_exp = 1;
-  }
   // Whole rounds on the persistent GEMM; a remainder that fits in the diagonal tail runs as
-  // strips (diag_strip_kernel) after it instead of as a third round / stream-K split. fp8 and
-  // exponential-store launches keep the stream-K schedule.
+  // strips (diag_strip_kernel) after it instead of as a third round / stream-K split. fp8
+  // launches keep the stream-K schedule.
   int nstrip = 0;
   const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
-  if (diag_tail > 0 && comp != DType::FP8 && !store_exp && diag_strips_enabled()) {
+  if (diag_tail > 0 && comp != DType::FP8 && diag_strips_enabled()) {
     const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
     if (q >= 1 && rem > 0 && rem <= diag_tail) nstrip = rem;
   }
   const int nmain = ntiles - nstrip;
   const int nk_tile = (int)(kb / kKStepBytes);
-  const int pieces = (!store_exp && part_x == nullptr) ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
+  const int pieces = part_x == nullptr ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
   int grid;
   if (pieces > 0) {  // split-K: every piece publishes its slab, sk_reduce_kernel finishes the tiles
     NTXENT_CHECK(kb % kKStepBytes == 0, "K not aligned to the K step");
@@ -1329,52 +1176,6 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-bool exp_backward_eligible(const Geometry& g, DType comp) {
-  const float M = g.inv_temp * dev::kLog2e;
-  return comp != DType::F32 && 2.0f * M < 120.0f && (long long)g.col_tiles * kTile <= dev::kExpMaxRows;
-}
-
-size_t exp_store_elems(const Geometry& g) {
-  const long long rt = g.row_tiles;
-  return (size_t)((rt * (rt + 1) / 2 + rt * (g.col_tiles - rt)) * kTileElems);
-}
-
-int exp_coef_shift(const Geometry& g) {
-  int s = 0;
-  while ((2LL << s) <= g.global_rows) ++s;  // floor(log2(2N))
-  return std::max(0, std::min(14, s - 3));
-}
-
-void launch_dz_exp(DType comp, const void* ebuf, const void* zqt_all, const float* lse2_all, const int4* tiles,
-                   int ntiles, void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                   bool out_f16) {
-  if (ntiles == 0) return;
-  const DType bc = backward_dtype(comp);
-  NTXENT_CHECK(exp_backward_eligible(g, comp), "dz_exp: plan not eligible for the exponential backward");
-  const long long cs = 2;
-  dev::SimParams p = base_params(g);
-  p.sc = const_cast<char*>(static_cast<const char*>(ebuf));
-  p.lse2 = lse2_all;
-  const int sh = exp_coef_shift(g);
-  p.a_shift = p.y_scale + (float)sh;
-  p.out_scale = std::ldexp(1.0f, -sh);
-  p.B.base = static_cast<const char*>(zqt_all);
-  p.B.ld = (long long)g.ld_t * cs;
-  p.B.row_tile_stride = (long long)kTile * g.ld_t * cs;
-  p.B.kblk = (long long)g.rows_pad * cs;
-  p.B.kblk_stride = (long long)g.dim_n * g.ld_t * cs;
-  p.tiles = tiles;
-  p.kbytes = (long long)g.world * g.rows_pad * cs;
-  p.out = static_cast<float*>(dz);
-  p.out_f16 = out_f16 ? 1 : 0;
-  p.ldo = g.dim_n;
-  p.slab_stride = (long long)g.rows_pad * g.dim_n;
-  const int grid = apply_schedule(p, ntiles, ws, stream);
-  if (bc == DType::BF16) launch_sim_gemm<__bf16, dev::kModeDzE>(grid, p, stream);
-  else launch_sim_gemm<_Float16, dev::kModeDzE>(grid, p, stream);
-  NTXENT_HIP_CHECK(hipGetLastError());
-}
-
 void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,
                     long long b_kblk_stride, int k_tiles, const int4* tiles, int ntiles, void* out, bool accum,
                     const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16) {
@@ -1412,14 +1213,8 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
 
 void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h, const float* inv,
                      const float* grad_out, void* dh, const Geometry& g, hipStream_t stream,
-                     const void* xslabs, int nx, const PosTerm& pos) {
+                     const void* xslabs, int nx) {
   const _Float16* xs = static_cast<const _Float16*>(xslabs);
-  dev::PosArgs pa{pos.zq, pos.cpos, pos.ld, 0, g.rows / 2};
-  if (pos.zq != nullptr) {
-    NTXENT_CHECK(pos.cpos != nullptr && (pos.zdt == DType::F16 || pos.zdt == DType::BF16) && pos.ld >= g.dim,
-                 "norm_bwd: bad positive-pair term");
-    pa.zdt = pos.zdt == DType::F16 ? 1 : 2;
-  }
   if (xs == nullptr) nx = 0;
   const float alpha_base = (float)(1.0 / ((double)g.global_rows * g.temperature));
   const long long ss = (long long)g.rows_pad * g.dim_n, ldo = g.dim_n;
@@ -1431,16 +1226,16 @@ void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h, co
     Tin* dp = static_cast<Tin*>(dh);
     if (vec && nch == 1)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 1>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec && nch == 2)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 2>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else if (vec)
       hipLaunchKernelGGL((dev::norm_bwd_vec_kernel<Tin, 4>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss,
-                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
+                         ldo, hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
     else
       hipLaunchKernelGGL((dev::norm_bwd_kernel<Tin>), dim3(g.rows), dim3(256), 0, stream, slabs, nslabs, ss, ldo,
-                         hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx, pa);
+                         hp, inv, grad_out, alpha_base, dp, g.dim, xs, nx);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

@@ -30,27 +30,7 @@
 namespace ntxent {
 namespace dev {
 
-enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2, kModeDzE = 3 };
-
-// Coefficient-free backward (kModeDzE): the forward keeps E = 2^(y - M) (bf16) instead of the
-// cosines, in slot exp_slot(...) of a triangular tile store, and the dZ GEMM forms
-// C = E * (a_i + a_j), a = 2^(M + s - lse2), while staging its A operand (see sim_gemm_kernel).
-constexpr int kExpTabLds = 32768;                   // a for up to 8192 global rows
-constexpr int kExpMaxRows = kExpTabLds / 4;
-constexpr int kExpMirror = 1 << 30;                 // exp_slot flag: stored tile is (J, I)
-// Slot of the stored exponential tile holding block (mt, J) of the local row tiles x global
-// column tiles (rt row tiles per rank, ct column tiles, own block at [t0, t0 + rt)): own block
-// upper triangle in row-major triangular order, then the remote tiles row by row. A lower own
-// tile (J < t0 + mt) is the transpose of the stored (J - t0, t0 + mt) tile: flag kExpMirror.
-__host__ __device__ __forceinline__ int exp_slot(int mt, int J, int rt, int ct, int t0) {
-  const int jl = J - t0;
-  if (jl >= 0 && jl < rt) {
-    const int lo = jl < mt ? jl : mt, hi = jl < mt ? mt : jl;
-    const int s = lo * rt - lo * (lo - 1) / 2 + (hi - lo);
-    return jl < mt ? (s | kExpMirror) : s;
-  }
-  return rt * (rt + 1) / 2 + mt * (ct - rt) + (J < t0 ? J : J - rt);
-}
+enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
 
 constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 64 KiB
 constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
@@ -91,11 +71,6 @@ struct SimParams {
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
-  int store_exp;         // forward: keep E = 2^(y - M) (bf16) in exp_slot order instead of cosines
-  float a_shift;         // kModeDzE: a = 2^(a_shift - lse2) (= M + s)
-  float out_scale;       // kModeDzE: 2^-s, applied to the accumulators before the store
-  int dbg;               // diagnostic ablations (NTXENT_GEMM_DEBUG; 0 in production)
-  unsigned long long* stamps;  // ABL & 32 diagnostic builds: s_memtime per barrier
   // persistent stream-K schedule (see sim_gemm_kernel)
   int nk;                // K-steps per tile
   int dp_tiles;          // whole-tile items processed in rounds of gridDim
@@ -112,17 +87,6 @@ struct SimParams {
 // each, MFMA C layout). Element offset of the unit = sc_unit(...) * 8. fp32 tiles keep one
 // fragment per 16-byte unit: (((rb >> 4) * 16 + (cb >> 4)) * 64 + lane) * 4.
 __device__ __forceinline__ int sc_unit(int rb, int cb, int lane) { return ((rb >> 4) * 8 + (cb >> 5)) * 64 + lane; }
-
-// Ablation bits (timing experiments only; results are garbage when set).
-constexpr int kDbgNoLoads = 1;     // skip the global->LDS staging in the main loop
-constexpr int kDbgNoStore = 2;     // forward: skip keeping the cosine tile
-constexpr int kDbgNoEpilogue = 4;  // skip every epilogue (accumulators kept live)
-// Production builds compile the runtime ablations out (p.dbg is always 0 there).
-#ifdef NTXENT_ABLATION_KERNELS
-constexpr bool kDbgBuild = true;
-#else
-constexpr bool kDbgBuild = false;
-#endif
 
 // One monotonically advancing K position of a staged half-tile stream (clamped at the last
 // K-step, so the trailing prefetches of the schedule re-read valid memory).
@@ -289,36 +253,22 @@ __device__ __forceinline__ f32x4 mma_mx_c(const i32x8& a, const i32x8& b, f32x4 
 // ------------------------------------------------------------------------------------
 // The similarity GEMM with its three epilogues (see the file header for the schedule).
 // ------------------------------------------------------------------------------------
-// ABL: compile-time ablations for diagnostic builds only (production instantiates ABL = 0):
-// 1 = no global->LDS DMA, 2 = no LDS operand reads, 4 = no MFMA, 8 = deeper DMA queue,
-// 16 = no barriers (8 and 16 only make sense with 2|4), 32 = clock stamps (tools/ablate_ct.sh).
 // FX: the forward epilogue's exponential form, fixed shift (1, tau > ~0.024) or per-tile max
 // (0). A compile-time choice: with both forms in one kernel the allocator spilled the main loop.
-template <typename T, int MODE, int ABL = 0, int FX = 1>
+template <typename T, int MODE, int FX = 1>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
   // fp8: 2 KiB more hold the dwords carrying the tile's 256 A-row and 256 B-row E8M0 scales (one
   // array: a second __shared__ object makes hipcc drain the LDS-DMA before every ds_read)
   constexpr int kScaleLds = MODE == kModeCoef ? kCoefLds : kGemmLds;
-  constexpr bool kDzE = MODE == kModeDzE;
-  // kModeDzE: 32 KiB more hold the table a[g] = 2^(a_shift - lse2[g]) of every global row
-  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + (std::is_same<T, fp8e4m3>::value ? 2048 : 0) +
-                                                    (kDzE ? kExpTabLds : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + (std::is_same<T, fp8e4m3>::value ? 2048 : 0)];
   lds_char* lds = (lds_char*)smem;
-  typedef __attribute__((address_space(3))) float lds_f;
-  typedef __attribute__((address_space(3))) f32x4 lds_f4;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wa = w >> 2, wb = w & 3;
   const int G = gridDim.x;
-  if constexpr (kDzE) {
-    lds_f* at = (lds_f*)(lds + kGemmLds);
-    const int n = p.col_tiles * kTile;  // <= kExpMaxRows (host-checked)
-    for (int g = tid; g < n; g += kGemmThreads) at[g] = fast_exp2(p.a_shift - p.lse2[g]);
-    __syncthreads();
-  }
   const int bid = xcd_remap(blockIdx.x, G);  // persistent block id (XCD-contiguous runs)
   const int nk = p.nk;                       // K-steps of a whole tile
   const char* Ab = nullptr;
@@ -340,12 +290,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
     const char* src = (isB ? Bb : Ab) + s.kbo + s.kin;
-    if (!(ABL & 1) && !(kDbgBuild && (p.dbg & kDbgNoLoads))) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
-                                         (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, 0);
-    }
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
+                                       (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, 0);
     s.advance(isB ? p.B : p.A);
   };
 
@@ -364,13 +312,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   typedef __attribute__((address_space(3))) const i32x4 lds_i4;
   OP af[NS][4], bf0[NS][2], bf1[NS][2];
   auto read_a = [&](int buf, int h, OP (&af)[NS][4]) {
-    if constexpr ((ABL & 2) != 0) {  // ablation: operands stay as they are, opaque to the compiler
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) asm volatile("" : "+v"(af[s][mi]));
-      return;
-    }
     const lds_char* As = lds + buf * kStageBytes;
     i32x4 lo[4];  // fp8: k-substep 0, joined with substep 1 into a fully (re)defined operand (a
                   // .lo/.hi partial write would keep the other half live across the whole kernel)
@@ -390,13 +331,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   };
   auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
-    if constexpr ((ABL & 2) != 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) asm volatile("" : "+v"(bf[s][ni]));
-      return;
-    }
     const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
     i32x4 lo[2];
 #pragma unroll
@@ -416,23 +350,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   };
   // s_setprio(1)/(0) around each MFMA cluster keeps hipcc from sinking the cluster across the
   // next s_barrier (cdna_hip_programming.md §5.5 T5).
-  auto no_fill = []() {};
-  // filler (kModeDzE): VALU work issued between the cluster's MFMAs (sched_group_barrier pattern
-  // below): beside MFMAs it costs little more than its issue slots
-  auto mma_quadrant = [&](auto qa_c, auto qb_c, OP (&af)[NS][4], OP (&bf)[NS][2], auto&& filler) {
+  auto mma_quadrant = [&](auto qa_c, auto qb_c, OP (&af)[NS][4], OP (&bf)[NS][2]) {
     constexpr int qa = decltype(qa_c)::value, qb = decltype(qb_c)::value;
-    constexpr bool kFill = !std::is_same<std::decay_t<decltype(filler)>, std::decay_t<decltype(no_fill)>>::value;
-    if constexpr ((ABL & 4) != 0) {  // ablation: consume the operands, issue no MFMA
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) asm volatile("" ::"v"(af[s][mi]));
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) asm volatile("" ::"v"(bf[s][ni]));
-      }
-      return;
-    }
-    if constexpr (kFill && (ABL & 512) != 0) filler();  // ablation: filler before the cluster
     __builtin_amdgcn_s_setprio(1);
     if constexpr (kF8) {
       // one block-scaled MFMA per (row block, column block) over the whole 128-element K-step
@@ -460,211 +379,25 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
           for (int ni = 0; ni < 2; ++ni) {
             f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
-            c = (MODE == kModeDz || kDzE) ? Mfma<T>::mma(bf[s][ni], af[s][mi], c) : Mfma<T>::mma(af[s][mi], bf[s][ni], c);
+            c = MODE == kModeDz ? Mfma<T>::mma(bf[s][ni], af[s][mi], c) : Mfma<T>::mma(af[s][mi], bf[s][ni], c);
           }
-      if constexpr (kFill && (ABL & (256 | 512)) == 0) {
-        filler();
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);  // then up to 8 VALU
-        }
-        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);    // the 2 LDS writes last
-      }
     }
     __builtin_amdgcn_s_setprio(0);
-    if constexpr (kFill && (ABL & 256) != 0) filler();  // ablation: filler after the cluster
   };
   const std::integral_constant<int, 0> kI0{};
   const std::integral_constant<int, 1> kI1{};
-  int n_stamp = 0;  // ABL & 32: clock stamp after every barrier of K-steps [4, 12), block 0
-  const bool stamper = (ABL & 32) && bid == 0 && lane == 0 && (w == 0 || w == 4);
   auto barrier = [&]() {
-    if constexpr ((ABL & 16) == 0) __builtin_amdgcn_s_barrier();  // ABL 16: no barriers (timing only)
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if constexpr ((ABL & 32) != 0) {
-      if (stamper && n_stamp < 256) p.stamps[(w >> 2) * 256 + n_stamp] = __builtin_amdgcn_s_memtime();
-      ++n_stamp;
-    }
   };
   auto lds_drain = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   // phase 1 issues the 8 A0 reads before the 4 B0 reads; LDS reads retire in order
   auto a0_retire = [&]() { asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); };
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
-  auto dma_wait = [&]() {
-    if constexpr ((ABL & 8) != 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // ABL 8: deeper queue (timing only)
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  };
+  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
   // Wave group (0: waves 0-3, 1: waves 4-7); each SIMD hosts one wave of each group.
   const int grp = __builtin_amdgcn_readfirstlane(w) >> 2;
-
-  // ---- kModeDzE: the A operand (C rows) is formed from the kept exponential tiles -------------
-  // A half-tile (128 rows of C x one 64-column K-step) = 16 groups of 64 canonical 16-byte units
-  // of ONE stored E tile: for a direct K-step (stored tile (I, J), J >= I) unit (row block 8h+w,
-  // column pair 2kk+c), for a mirrored one (stored (J, I)) unit (row block 4kk+2(w&1)+c, column
-  // pair 4h+(w>>1)) -- wave w stages groups 2w+c (c = 0, 1), 1 KiB each, by LDS-DMA. Four phases
-  // later the same wave transforms its own units IN PLACE: C = E * (a_rho + a_kappa) from the
-  // LDS table, converted to T and written back to a bank-swizzled slot of the unit
-  // (slot 16q + (k ^ 4(q&1)), 8-byte halves swapped for q >= 2; lane 16q + k of a unit holds
-  // rows 4q..4q+3 of columns k and k+16). The MMA waves read the fragments with
-  // ds_read_b64_tr_b16 (direct: 4 consecutive columns of one row) or ds_read_b64 (mirrored:
-  // the unit already holds 4 consecutive rows of one column), both conflict-free.
-  int e_mt = 0, e_kb = 0, e_ns = 1;  // current item: row tile, first K-step, K-steps
-  auto e_pos = [&](int t, int& slot, bool& mir, int& kk, int& J) {
-    const int gk = e_kb + (t < e_ns ? t : e_ns - 1);  // clamped like KStream
-    J = gk >> 2;
-    kk = gk & 3;
-    const int e = exp_slot(e_mt, J, p.Rpad / kTile, p.col_tiles, p.row_tile0);
-    mir = (e & kExpMirror) != 0;
-    slot = e & (kExpMirror - 1);
-  };
-  auto stage_e = [&](int h, int t, int buf) {
-    int slot, kk, J;
-    bool mir;
-    e_pos(t, slot, mir, kk, J);
-    const char* tile = p.sc + (long long)slot * (kTileElems * 2);
-    lds_char* dst = lds + buf * kStageBytes + h * kHalfBytes + w * 2048;
-    if constexpr ((ABL & 1) != 0) return;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int rbi = mir ? 4 * kk + 2 * (w & 1) + c : 8 * h + w;
-      const int cbi = mir ? 4 * h + (w >> 1) : 2 * kk + c;
-      __builtin_amdgcn_global_load_lds((const void*)(tile + ((rbi * 8 + cbi) * 64 + lane) * 16),
-                                       (lds_void*)(dst + c * 1024), 16, 0, 0);
-    }
-  };
-  // transform, part 1 (load interval): this wave's two raw units and their a values
-  struct XLoad {
-    u32x4 raw[2];
-    f32x4 ar[2];
-    float ak[2][2];
-  };
-  auto xload = [&](int h, int t, int buf) {
-    XLoad x{};
-    if constexpr (kDzE && (ABL & 128) == 0) {  // ABL 128: no transform (timing only)
-      int slot, kk, J;
-      bool mir;
-      e_pos(t, slot, mir, kk, J);
-      (void)slot;
-      const lds_char* base = lds + buf * kStageBytes + h * kHalfBytes + w * 2048;
-      const lds_f* at = (const lds_f*)(lds + kGemmLds);
-      const int q = lane >> 4, k = lane & 15;
-      const int iside = p.own0 + e_mt * kTile, jside = J * kTile;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        x.raw[c] = *(const lds_u4*)(base + c * 1024 + lane * 16);
-        const int rho = mir ? jside + 16 * (4 * kk + 2 * (w & 1) + c) + 4 * q : iside + 16 * (8 * h + w) + 4 * q;
-        const int kap = mir ? iside + 32 * (4 * h + (w >> 1)) + k : jside + 64 * kk + 32 * c + k;
-        x.ar[c] = *(const lds_f4*)(at + rho);
-        x.ak[c][0] = at[kap];
-        x.ak[c][1] = at[kap + 16];
-      }
-    }
-    return x;
-  };
-  // part 2 (compute interval, between MFMAs): C = E (a_rho + a_kappa) in T, written back in place
-  // to the swizzled slot
-  auto xstore = [&](int h, int buf, const XLoad& x) {
-    if constexpr (kDzE && (ABL & 128) == 0) {
-      lds_char* base = lds + buf * kStageBytes + h * kHalfBytes + w * 2048;
-      const int q = lane >> 4, k = lane & 15;
-      u32x4 o[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {  // dword d: rows 2(d&1), 2(d&1)+1 of column k + 16(d>>1)
-          const unsigned e2 = x.raw[c][d];
-          const float lo = __uint_as_float(e2 << 16), hi = __uint_as_float(e2 & 0xffff0000u);
-          union { T h[2]; unsigned u; } pk;
-          pk.h[0] = from_f32<T>(lo * (x.ar[c][2 * (d & 1)] + x.ak[c][d >> 1]));
-          pk.h[1] = from_f32<T>(hi * (x.ar[c][2 * (d & 1) + 1] + x.ak[c][d >> 1]));
-          o[c][d] = pk.u;
-        }
-        if (q >= 2) o[c] = __builtin_shufflevector(o[c], o[c], 2, 3, 0, 1);
-      }
-      const int ps = (16 * q + (k ^ (4 * (q & 1)))) * 16;
-      *(lds_u4*)(base + ps) = o[0];
-      *(lds_u4*)(base + 1024 + ps) = o[1];
-    }
-  };
-  // fragment read offsets (bytes inside a unit group / half-tile), see above; recomputed per
-  // call (a few VALU) rather than held across the loop (the registers are the binding limit)
-  auto e_offsets = [&](int (&offD)[2], int (&offM)[2][2]) {
-    int l = lane;
-    asm volatile("" : "+v"(l));  // opaque: keeps the lane math out of the persistent loop's live set
-    const int lg = l >> 4, l16 = l & 15, qD = l16 & 3, hD = lg >> 1;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int kD = 8 * (lg & 1) + 4 * t + (l16 >> 2);
-      offD[t] = 16 * (16 * qD + (kD ^ (4 * (qD & 1)))) + 8 * (hD ^ (qD >> 1));
-      const int qM = 2 * (lg & 1) + t;
-#pragma unroll
-      for (int hm = 0; hm < 2; ++hm)
-        offM[hm][t] = (lg >> 1) * 1024 + 16 * (16 * qM + (l16 ^ (4 * (qM & 1)))) + 8 * (hm ^ (qM >> 1));
-    }
-  };
-  typedef short v4s __attribute__((ext_vector_type(4)));
-  typedef short v8s __attribute__((ext_vector_type(8)));
-  typedef __attribute__((address_space(3))) v4s lds_v4s;
-  // The two 8-byte halves of each A fragment land in ah[.][.][0/1] and are joined into af only
-  // after the interval's explicit LDS drain (e_join): the transposed reads are issued by inline
-  // asm, whose results the compiler does not track -- as a builtin, hipcc preceded every group of
-  // them with a full vmcnt(0) drain of the in-flight LDS-DMA (it cannot disambiguate the builtin's
-  // LDS access), which doubled the K-step.
-  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
-  u32x2v ah[NS][4][2];
-  auto read_a_e = [&](int buf, int h, int t) {
-    if constexpr (kDzE && (ABL & 2) != 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) asm volatile("" : "+v"(ah[s][mi][0]), "+v"(ah[s][mi][1]));
-    } else if constexpr (kDzE) {
-      int slot, kk, J;
-      bool mir;
-      e_pos(t, slot, mir, kk, J);
-      const lds_char* As = lds + buf * kStageBytes + h * kHalfBytes;
-      int offD[2], offM[2][2];
-      e_offsets(offD, offM);
-      if constexpr ((ABL & 1024) != 0) mir = true;   // ablation: every K-step read as mirrored
-      if constexpr ((ABL & 2048) != 0) mir = false;  // ablation: every K-step read as direct
-      if (!mir) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) {
-            const lds_char* u = As + (2 * (4 * wa + mi) + s) * 1024;
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {
-              const unsigned addr = (unsigned)(uintptr_t)(u + offD[tt]);
-              asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(ah[s][mi][tt]) : "v"(addr));
-            }
-          }
-      } else {
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int mi = 0; mi < 4; ++mi) {
-            const lds_char* u = As + 2 * (2 * (2 * wa + (mi >> 1)) + s) * 1024;
-#pragma unroll
-            for (int tt = 0; tt < 2; ++tt) {  // asm: hipcc merged pairs into ds_read2_b64 (4-way conflicts)
-              const unsigned addr = (unsigned)(uintptr_t)(u + offM[mi & 1][tt]);
-              asm volatile("ds_read_b64 %0, %1" : "=v"(ah[s][mi][tt]) : "v"(addr));
-            }
-          }
-      }
-    }
-  };
-  auto e_join = [&](OP (&af)[NS][4]) {  // after an lgkmcnt(0) drain
-    if constexpr (kDzE) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
-          af[s][mi] = __builtin_bit_cast(OP, (u32x4)__builtin_shufflevector(ah[s][mi][0], ah[s][mi][1], 0, 1, 2, 3));
-    }
-  };
 
   // Each K-step: 4 phases (C-quadrants), each split into a load interval L (re-stage one
   // half-tile, read this phase's operands into registers, drain the reads) and a compute
@@ -693,24 +426,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const long long it1 = it0 + p.ipb < sk_total ? it0 + p.ipb : sk_total;
   const int n_dp = p.dp_tiles > bid ? (p.dp_tiles - bid + G - 1) / G : 0;
   long long it = it0;
-  // ABL & 64: per-block item timeline (diagnostic builds). 64 slots per block: [0] memtime and
-  // [1] memrealtime at entry, [2]/[3] the same at exit; item k at 4 + 6k: tile, K-steps, then
-  // memtime at item start, main-loop end, stream-K fixup end, epilogue end.
-  unsigned long long* tl = (ABL & 64) ? p.stamps + (size_t)bid * 64 : nullptr;
-  // (the clock reads happen only inside the constexpr branch: production code is unchanged)
-  auto tval = [&](int slot, unsigned long long v) {
-    if constexpr ((ABL & 64) != 0) {
-      if (threadIdx.x == 0 && slot < 64) tl[slot] = v;
-    }
-  };
-  auto tstamp = [&](int slot) {
-    if constexpr ((ABL & 64) != 0) tval(slot, __builtin_amdgcn_s_memtime());
-  };
-  if constexpr ((ABL & 64) != 0) tval(1, __builtin_amdgcn_s_memrealtime());
-  tstamp(0);
   for (int item = 0;; ++item) {
   int tile, kb, ke, stile = -1;
-  long long seg0 = 0;
   if (item < n_dp) {
     tile = bid + item * G;
     kb = 0;
@@ -720,16 +437,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     stile = (int)(it / nk);
     kb = (int)(it % nk);
     ke = (int)((long long)kb + (it1 - it) < nk ? kb + (it1 - it) : nk);
-    seg0 = it;
     it += ke - kb;
     tile = p.dp_tiles + stile;
   }
   const int4 t = p.tiles[tile];
   const int mt = t.x, nt = t.y;
   const int nsteps = ke - kb;
-  tval(4 + 6 * item, (unsigned long long)tile);
-  tval(5 + 6 * item, (unsigned long long)nsteps);
-  tstamp(6 + 6 * item);
   Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
   Bb = p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride;
   {
@@ -742,63 +455,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  e_mt = mt;
-  e_kb = kb;
-  e_ns = nsteps;
-  if constexpr (kDzE) {
-    // A0(t+2) is DMA'd in phase 2 and A1(t+2) in phase 4 of step t (one phase after the last read
-    // of the buffer, which retires before the barrier, as for A0 below). A1(t) is transformed in
-    // phase 1 of step t and A0(t+1) in phase 4 -- the two compute intervals with the fewest live
-    // operand registers -- loads in the L interval, arithmetic and the two LDS writes between the
-    // MFMAs of the C interval; five and six phases after the DMA was issued.
-    // Prologue: A0(0) staged and transformed; then B0(0) B1(0) A1(0) A0(1) B0(1) B1(1) A1(1) in
-    // flight -- the issue order the counted waits of the loop assume.
-    stage_e(0, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    {
-      const XLoad x0 = xload(0, 0, 0);
-      xstore(0, 0, x0);
-    }
-    stage(1, 0, sb0, 0); stage(1, 1, sb1, 0);
-    stage_e(1, 0, 0);
-    stage_e(0, 1, 1);
-    stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
-    stage_e(1, 1, 1);
-    barrier();
-    if (grp == 1) barrier();
-    for (int ks = 0; ks < nsteps; ++ks) {
-      const int cur = ks & 1, nxt = cur ^ 1;
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A1(t), B0(t), B1(t) landed
-      lds_drain();                    // and the A0(t) writes of the previous phase 4
-      barrier();                      // phase 1 L
-      const XLoad x1 = xload(1, ks, cur);
-      read_a_e(cur, 0, ks);
-      __builtin_amdgcn_sched_barrier(0);
-      read_b(cur, 0, bf0);
-      a0_retire(); barrier();         // phase 1 C (A0 is restaged next phase)
-      lds_drain();
-      e_join(af);
-      mma_quadrant(kI0, kI0, af, bf0, [&]() { xstore(1, cur, x1); });
-      barrier();                      // phase 2 L
-      read_b(cur, 1, bf1);
-      stage_e(0, ks + 2, cur);        //   A0 of step ks+2
-      barrier(); lds_drain();         // phase 2 C (also retires the A1(t) writes)
-      mma_quadrant(kI0, kI1, af, bf1, no_fill);
-      barrier();                      // phase 3 L
-      read_a_e(cur, 1, ks);
-      stage(1, 0, sb0, cur);          //   B0 of step ks+2
-      lds_drain(); barrier();         // phase 3 C: A1 is restaged next phase -> reads retire first
-      e_join(af);
-      mma_quadrant(kI1, kI0, af, bf0, no_fill);
-      barrier();                      // phase 4 L
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // this wave's A0(t+1) pieces landed
-      const XLoad x0 = xload(0, ks + 1, nxt);
-      stage(1, 1, sb1, cur);          //   B1 of step ks+2
-      stage_e(1, ks + 2, cur);        //   A1 of step ks+2
-      barrier();                      // phase 4 C
-      mma_quadrant(kI1, kI1, af, bf1, [&]() { xstore(0, nxt, x0); });
-    }
-  } else {
   // prologue: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1 (the stream clamps keep the
   // trailing prefetches in bounds, so every wait count below is uniform)
   if constexpr (kF8) {
@@ -823,23 +479,22 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     stage(0, 1, sa1, nxt);          //   A1 of step ks+1
     a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
     lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
-    mma_quadrant(kI0, kI0, af, bf0, no_fill);
+    mma_quadrant(kI0, kI0, af, bf0);
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
     read_b(cur, 1, bf1);
     stage(0, 0, sa0, cur);          //   A0 of step ks+2
     barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
-    mma_quadrant(kI0, kI1, af, bf1, no_fill);
+    mma_quadrant(kI0, kI1, af, bf1);
     barrier();                      // phase 3 L
     read_a(cur, 1, af);
     stage(1, 0, sb0, cur);          //   B0 of step ks+2
     barrier(); lds_drain();         // phase 3 C (A1 is restaged two phases later)
-    mma_quadrant(kI1, kI0, af, bf0, no_fill);
+    mma_quadrant(kI1, kI0, af, bf0);
     dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
     barrier();                      // phase 4 C
-    mma_quadrant(kI1, kI1, af, bf1, no_fill);
+    mma_quadrant(kI1, kI1, af, bf1);
   }
-  }  // !kDzE
   if (grp == 0) barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
   if constexpr (kF8) {
@@ -864,7 +519,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
 
   __syncthreads();
-  tstamp(7 + 6 * item);
   {
   // Thread indices re-derived through an opaque copy: keeps the compiler from hoisting the
   // epilogue's address arithmetic out of the persistent loop, where it would stay live across
@@ -895,7 +549,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       const bool first_partial = (s / nk == stile) && (s % nk != 0);
       return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
     };
-    (void)seg0;
     const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
     const unsigned lane_off = (unsigned)((w * 32 * 64 + lane) * 16);
     {
@@ -909,7 +562,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     __syncthreads();
     if (p.sk_out) {  // split-K forward: the reduce launch finishes the tile
-      tstamp(8 + 6 * item);
       continue;
     }
     int* flag = reinterpret_cast<int*>(smem);
@@ -924,7 +576,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const bool last = flag[0] != 0;
     __syncthreads();
     if (!last) {
-      tstamp(8 + 6 * item);
       continue;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
@@ -989,25 +640,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       }
     }
   }
-  tstamp(8 + 6 * item);
 
-  if (kDbgBuild && (p.dbg & kDbgNoEpilogue)) {  // timing ablation: keep the MFMA results live, write nothing
-    float s = 0.f;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) s += acc[mi][ni][0] + acc[mi][ni][3];
-    if (s == 1.2345e-30f) p.part[tid] = make_float2(s, s);
-  } else if constexpr (MODE == kModeDz || kDzE) {
+  if constexpr (MODE == kModeDz) {
     // swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r]
-    if constexpr (kDzE) {  // undo the 2^s of the coefficient table
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] *= p.out_scale;
-    }
     float* out = p.out;
-    if (!kDzE && p.out_f16 && !p.accum) {
+    if (p.out_f16 && !p.accum) {
       // fp16 tile through LDS (free after the main loop): fragments -> row-major [256][256] with
       // the 16-byte chunk index XORed by (row & 15) (conflict-free both ways), then 512-byte
       // coalesced rows out. A fragment's direct 8-byte stores put 16 rows in every instruction.
@@ -1055,7 +692,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
     const int kind = t.z;
-    if (p.sc && !p.store_exp && !(kDbgBuild && (p.dbg & kDbgNoStore))) {  // keep cosines (compact slot per tile, canonical order)
+    if (p.sc) {  // keep cosines (compact slot per tile, canonical order)
       typedef typename StoreT<T>::type TS;
       TS* st = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
       const float cs = p.cos_scale;
@@ -1094,7 +731,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const bool col_out = kind == kTileSymOff || kind == kTileCross;  // column partials too
     constexpr bool fixed = FX != 0;  // launch_sim_gemm picks FX = p.fixed_shift
     const float M = p.y_scale;
-    if (item < 6) tstamp(40 + 4 * item);  // ABL & 64: epilogue phases (cosines stored)
     // Masks, as a pre-pass that sets the masked raw values to -inf (exp2 -> 0). Element
     // (tile row tr, tile col tc) is the self pair when tc - tr == r0 - c0 and a positive when
     // tc - tr == r0 - c0 +- n_half; a 16x16 fragment can hold such an element only if its block
@@ -1138,7 +774,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           }
       }
     }
-    if (item < 6) tstamp(41 + 4 * item);  // masks applied
     const float sc_ = p.acc_scale;
     float2* rowred = reinterpret_cast<float2*>(smem);                // [4 wb][256]
     float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2 wa][256]
@@ -1147,30 +782,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       // reduce the 4 rows, fold into the column sums; acc[mi] is dead afterwards, which keeps
       // the epilogue's register footprint at the accumulators'.
       float csum[4] = {0.f, 0.f, 0.f, 0.f};
-      // store_exp: the exponentials themselves are kept (bf16, canonical order, exp_slot tile
-      // order): masked elements (self, positive, padding) are exactly 0
-      __bf16* est = nullptr;
-      if (p.store_exp)
-        est = reinterpret_cast<__bf16*>(p.sc) +
-              (long long)exp_slot(mt, nt, p.Rpad / kTile, p.col_tiles, p.row_tile0) * kTileElems;
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fast_exp2(acc[mi][ni][r] * sc_ - M);
-        if (est) {
-#pragma unroll
-          for (int np = 0; np < 2; ++np) {
-            union { __bf16 h[8]; u32x4 u; } pk;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              pk.h[r] = (__bf16)acc[mi][2 * np][r];
-              pk.h[4 + r] = (__bf16)acc[mi][2 * np + 1][r];
-            }
-            *reinterpret_cast<u32x4*>(est + sc_unit(rb[mi], cb[2 * np], lane) * 8) = pk.u;
-          }
-        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
@@ -1229,9 +846,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         }
       }
     }
-    if (item < 6) tstamp(42 + 4 * item);  // exponentials and wave reductions done
     __syncthreads();
-    if (item < 6) tstamp(43 + 4 * item);
     if (tid < 256) {
       float2 v = rowred[tid];
       float m = v.x, s = v.y;
@@ -1257,10 +872,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
   }  // epilogue scope
   __syncthreads();  // LDS of this item's epilogue is reused by the next item's staging
-  tstamp(9 + 6 * item);
   }  // work items
-  tstamp(2);
-  if constexpr ((ABL & 64) != 0) tval(3, __builtin_amdgcn_s_memrealtime());
 }
 
 // Store-mode coefficient pass: one wave per 64x64 region (wm, wn, half) of a kept cosine tile

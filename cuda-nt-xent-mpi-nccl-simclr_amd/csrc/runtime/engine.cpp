@@ -38,7 +38,6 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   bwd_ = backward_dtype(cfg.compute);
   cs_ = dtype_size(bwd_);
   small_ = cfg.small_path && world_ == 1 && small_path_eligible(g_, cfg.compute);
-  exp_ = !small_ && cfg_.keep_cos && cfg.exp_backward && exp_backward_eligible(g_, cfg.compute);
 
   const auto ft = build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -57,8 +56,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&inv_, R * 4},
       {(void**)&ypos_, R * 4},
       {(void**)&part_, (size_t)g_.col_tiles * Rp * sizeof(float2)},
-      {(void**)&sbuf_, exp_ ? exp_store_elems(g_) * 2 : cfg_.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
-      {(void**)&cbuf_, exp_ ? 0 : (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
+      {(void**)&sbuf_, cfg_.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
+      {(void**)&cbuf_, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
       {(void**)&lse2_all_, W * Rp * 4},
       {(void**)&cpos_, Rp * 4},
       {(void**)&block_loss_, (size_t)lse_scratch_floats(g_) * 4},
@@ -146,15 +145,13 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s, BlockView{},
-                     nullptr, exp_, own_diag_tail(g_));
+                     nullptr, own_diag_tail(g_));
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");
     if (world_ > 1) NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zq_, 0));
-    // (the exponential store places tiles by exp_slot itself: same base pointer)
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
-                     exp_ ? sbuf_ : sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_ovl, g_, s,
-                     BlockView{}, nullptr, exp_);
+                     sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_ovl, g_, s);
   }
   {
     NTXENT_TRACE("ntxent.lse");
@@ -180,26 +177,6 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     fault_point("dz");
     launch_small_bwd(cfg_.input, cfg_.compute, zq_local, h_, inv_, lse2_all_, cpos_, grad_out ? grad_out : one_, dh,
                      small_scratch_, g_, s, std::min(cfg_.small_splits, small_rows_pad(g_) / 64));
-    return;
-  }
-  if (exp_) {  // coefficient-free: C is formed inside the dZ GEMM from the kept exponentials
-    if (zqt_pending_) {
-      NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));
-      zqt_pending_ = false;
-    }
-    {
-      NTXENT_TRACE("ntxent.dz_gemm");
-      fault_point("dz");
-      launch_dz_exp(cfg_.compute, sbuf_, zqt_all_, lse2_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true);
-    }
-    NTXENT_TRACE("ntxent.norm_bwd");
-    fault_point("norm_bwd");
-    PosTerm pos;
-    pos.zq = zq_local;
-    pos.zdt = bwd_;
-    pos.ld = g_.ld_k;
-    pos.cpos = cpos_;
-    launch_norm_bwd(cfg_.input, nullptr, 0, h_, inv_, grad_out ? grad_out : one_, dh, g_, s, slabs_, 1, pos);
     return;
   }
   {

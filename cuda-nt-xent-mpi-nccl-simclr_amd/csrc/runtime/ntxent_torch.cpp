@@ -15,6 +15,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <atomic>
@@ -65,8 +66,6 @@ struct Plan {
   int n_dz = 0;
   int num_cus = 256;
   bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
-  // coefficient-free backward: the single-process flow keeps exponentials (exp_backward_eligible)
-  bool exp_bwd = false;
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
@@ -115,7 +114,6 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
   p->small = small_path_eligible(p->g, comp);
-  p->exp_bwd = exp_backward_eligible(p->g, comp);
   cache.emplace(key, p);
   return p;
 }
@@ -129,42 +127,34 @@ static void check_input(const at::Tensor& h, const char* name) {
   NTXENT_CHECK(h.is_contiguous(), std::string(name) + " must be contiguous");
 }
 
-// Coefficient-free backward switch (off by default while its dZ GEMM is slower than the
-// coefficient pass + dZ GEMM it replaces; see tests/test_gpu_expbwd.py, profiles/r2/expbwd).
-static std::atomic<bool> g_exp_backward{false};
-void set_exp_backward(bool on) { g_exp_backward = on; }
-bool exp_backward_enabled() { return g_exp_backward.load(); }
-
 static at::TensorOptions opts(const at::Tensor& like, at::ScalarType t) {
   return at::TensorOptions().dtype(t).device(like.device());
 }
 
-// Zero-initialised per-device scratch for the kernels' self-cleaning arrival counters
-// (stream-K tile arrivals, LSE last-block-done). Every launch returns its counters to zero, so
-// a buffer is zeroed only when it is (re)allocated, and no memset runs per launch. Launches
-// sharing a slot are stream-ordered (every op enqueues on the current stream; ops of one
-// device run on one stream in the autograd and data-parallel paths). A grown buffer replaces
-// the old one; the caching allocator keeps the old block alive until its stream is done.
+// Zero-initialised scratch for the kernels' self-cleaning arrival counters (stream-K tile
+// arrivals, LSE and small-path last-block-done tickets) and their partials. Every launch returns
+// its counters to zero, so a buffer is zeroed only when it is (re)allocated and no memset runs
+// per launch. The cache is keyed by (device, slot, STREAM): launches sharing one buffer are then
+// always stream-ordered, and losses evaluated concurrently on different streams never race on
+// one ticket (a counter reset in the middle of another stream's launch would leave it non-zero
+// and starve every later last-arriver). A grown buffer replaces the old one; the caching
+// allocator keeps the old block alive until its stream is done.
 static at::Tensor device_scratch(const at::Tensor& like, size_t bytes, int slot) {
   static std::mutex mu;
-  static std::map<std::pair<int, int>, at::Tensor> cache;
+  static std::map<std::tuple<int, int, hipStream_t>, at::Tensor> cache;
   std::lock_guard<std::mutex> lock(mu);
-  auto& t = cache[{(int)like.device().index(), slot}];
+  auto& t = cache[{(int)like.device().index(), slot, cur_stream(like)}];
   if (!t.defined() || (size_t)t.numel() < bytes) t = at::zeros({(long)bytes}, opts(like, at::kByte));
   return t;
 }
 
 
-// CUs left free for communication kernels by the GEMMs launched while it is non-zero (the
-// data-parallel paths set it around launches that overlap an RCCL transfer; see
-// parallel/commstats.py:comm_overlap).
-static std::atomic<int> g_grid_reserve{0};
-int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
-
+// CUs left free for communication kernels: set_grid_reserve (ntxent.h), see
+// parallel/commstats.py:comm_overlap.
 static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
   GemmWorkspace ws;
   ws.num_cus = P.num_cus;
-  ws.sched_cus = std::max(1, P.num_cus - std::min(g_grid_reserve.load(), P.num_cus / 2));
+  ws.sched_cus = std::max(1, P.num_cus - std::min(grid_reserve(), P.num_cus / 2));
   ws.bytes = gemm_workspace_bytes(ntiles, P.num_cus);
   ws.ptr = device_scratch(like, ws.bytes, 0).data_ptr();
   return ws;
@@ -224,7 +214,7 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
 }
 
 std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P,
-                                  bool keep_cos, bool store_exp = false, hipEvent_t main_done = nullptr) {
+                                  bool keep_cos) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.op_ld(),
@@ -232,16 +222,13 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  // the exponential store is returned 3-D [slots, 256, 256] (cosines: flat), which is how the
-  // backward tells the two apart
-  if (store_exp) sc = at::empty({(long)(exp_store_elems(P.g) / kTileElems), kTile, kTile}, opts(zq_local, at::kBFloat16));
-  else if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), sc.defined() ? sc.data_ptr() : nullptr,
-                   ws, P.g, cur_stream(zq_local), BlockView{}, nullptr, store_exp,
-                   P.n_fwd == P.n_own ? own_diag_tail(P.g) : 0, main_done);
+                   ws, P.g, cur_stream(zq_local), BlockView{}, nullptr,
+                   P.n_fwd == P.n_own ? own_diag_tail(P.g) : 0);
   return {part, sc};
 }
 
@@ -267,7 +254,7 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
-                   nullptr, false, first + count == P.n_own ? std::min(count, own_diag_tail(P.g)) : 0);
+                   nullptr, first + count == P.n_own ? std::min(count, own_diag_tail(P.g)) : 0);
 }
 
 // Writes this rank's slice of lse2_all (log2 units) and cpos (the positive coefficient
@@ -336,46 +323,15 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   return slabs;
 }
 
-// Exponential store (fwd_stats store_exp) -> dZ without the positive pair (fp16 slab), see
-// launch_dz_exp; norm_bwd(..., zq, cpos) adds it back.
-at::Tensor dz_exp(const at::Tensor& ebuf, const at::Tensor& zqt_all, const at::Tensor& lse2_all, const Plan& P) {
-  check_input(ebuf, "ebuf");
-  check_input(zqt_all, "zqt_all");
-  NTXENT_CHECK(P.exp_bwd, "dz_exp: plan is not eligible for the exponential backward");
-  NTXENT_CHECK(ebuf.numel() == (long)exp_store_elems(P.g) && ebuf.scalar_type() == at::kBFloat16,
-               "ebuf must be the bf16 exponential store of the plan");
-  NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
-  NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad, "lse2_all must be [world*rows_pad]");
-  const at::DeviceGuard guard(ebuf.device());
-  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(ebuf, at::kHalf));
-  auto ws = gemm_ws(ebuf, P.n_dz, P);
-  launch_dz_exp(P.comp, ebuf.data_ptr(), zqt_all.data_ptr(), lse2_all.data_ptr<float>(),
-                reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws, P.g,
-                cur_stream(ebuf), /*out_f16=*/true);
-  return slabs;
-}
-
 at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tensor& inv, const at::Tensor& grad_out,
-                    const Plan& P, const c10::optional<at::Tensor>& zq_pos_in = c10::nullopt,
-                    const c10::optional<at::Tensor>& cpos_in = c10::nullopt) {
-  const at::Tensor zq_pos = zq_pos_in.has_value() ? *zq_pos_in : at::Tensor();
-  const at::Tensor cpos = cpos_in.has_value() ? *cpos_in : at::Tensor();
+                    const Plan& P) {
   check_input(h, "h");
   const at::DeviceGuard guard(h.device());
   auto go = grad_out.to(at::kFloat).contiguous();
   auto dh = at::empty_like(h);
-  PosTerm pos;
-  if (zq_pos.defined()) {  // exponential backward: the positive pair's term
-    NTXENT_CHECK(cpos.defined() && cpos.numel() >= P.g.rows && zq_pos.numel() >= (long)P.g.rows * P.g.ld_k,
-                 "norm_bwd: positive term needs zq [rows_pad, ld_k] and cpos");
-    pos.zq = zq_pos.data_ptr();
-    pos.zdt = to_dtype(zq_pos.scalar_type());
-    pos.ld = P.g.ld_k;
-    pos.cpos = cpos.data_ptr<float>();
-  }
   if (slabs.scalar_type() == at::kHalf)  // one fp16 dZ slab (dz() of a reduced-precision plan)
     launch_norm_bwd(to_dtype(h.scalar_type()), nullptr, 0, h.data_ptr(), inv.data_ptr<float>(), go.data_ptr<float>(),
-                    dh.data_ptr(), P.g, cur_stream(h), slabs.data_ptr(), 1, pos);
+                    dh.data_ptr(), P.g, cur_stream(h), slabs.data_ptr(), 1);
   else
     launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
                     go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
@@ -493,7 +449,7 @@ void fwd_stats_sym(const at::Tensor& zq_local, const at::Tensor& zq_all, const a
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), tp + first, count,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
-                   reinterpret_cast<float2*>(part_x.data_ptr<float>()), false,
+                   reinterpret_cast<float2*>(part_x.data_ptr<float>()),
                    first + count == P.n_own ? std::min(count, own_diag_tail(P.g)) : 0);
 }
 
@@ -601,18 +557,13 @@ at::Tensor norm_bwd_slabs(const at::Tensor& slabs, const at::Tensor& h, const at
 }
 
 // ---- single-process fused flows ------------------------------------------------------
-// Small-problem path switch (default on): the one-launch forward / backward of
-// small_kernels.hip for plans with Plan::small; off = the large-problem pipeline for every
-// shape (A/B tests and benchmarks).
-static bool g_small_path = true;
-static int g_small_splits = 0;  // backward column splits (0: small_bwd_splits)
-void set_small_path(bool on) { g_small_path = on; }
-bool small_path_enabled() { return g_small_path; }
-void set_small_splits(int n) { g_small_splits = std::max(0, n); }
+// Small-problem path (set_small_path, default on): the one-launch forward / backward of
+// small_kernels.hip for plans with Plan::small.
 
 static int small_splits(const Plan& P) {
   const int nt = small_rows_pad(P.g) / 64;
-  return g_small_splits > 0 ? std::min(g_small_splits, nt) : small_bwd_splits(P.g);
+  const int o = small_splits_override();
+  return o > 0 ? std::min(o, nt) : small_bwd_splits(P.g);
 }
 static at::Tensor small_scratch(const at::Tensor& like, const Plan& P) {
   return device_scratch(like, small_scratch_bytes(P.g, std::max(small_splits(P), small_bwd_splits(P.g))), 2);
@@ -629,7 +580,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
-  if (P->small && g_small_path) {
+  if (P->small && small_path_enabled()) {
     // {loss, zq, -, inv, lse2, -, a}: the backward recomputes S from zq (small_bwd)
     const int rp = small_rows_pad(P->g);
     auto lse2 = at::empty({rp}, opts(h, at::kFloat));
@@ -647,10 +598,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
-  // plans eligible for the coefficient-free backward keep exponentials instead of cosines
-  const bool keep = keep_cos || f8;
-  const bool ex = P->exp_bwd && g_exp_backward.load();
-  auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true, ex) : fwd_stats(pr[0], pr[0], *P, keep, keep && ex);
+  auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   auto loss = lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
@@ -675,10 +623,6 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     return dh;
   }
   at::Tensor cb;
-  if (sc_in.has_value() && sc_in->defined() && sc_in->dim() == 3) {  // kept exponentials: no coefficient pass
-    auto slabs = dz_exp(*sc_in, zqt, lse2, *P);
-    return norm_bwd(slabs, h, inv, grad_out, *P, zq, cpos);
-  }
   if (sc_in.has_value() && sc_in->defined()) {
     cb = coef(*sc_in, lse2, cpos, *P);
   } else {
@@ -694,23 +638,67 @@ at::Tensor forward_op(const at::Tensor& z, double T, bool use_mixed_precision) {
   return out[0];
 }
 
+// Row statistics handed from forward_with_stats to backward. The backward trusts a caller's LSE
+// only when it is exactly a tensor forward_with_stats returned, unmodified since, for the SAME z
+// tensor (same TensorImpl, same version counter: no in-place update in between), the same T and
+// the same precision; anything else (the reference's softmax, an empty tensor, a stale LSE from
+// an earlier step or another temperature) makes the backward recompute the statistics, so a
+// result never silently depends on stale caller-provided stats.
+namespace {
+struct StatsTag {
+  c10::weak_intrusive_ptr<c10::TensorImpl> stats, z;
+  int64_t stats_ver = 0, z_ver = 0;
+  double T = 0.0;
+  bool mp = false;
+};
+std::mutex g_tag_mu;
+std::vector<StatsTag> g_tags;  // most recent last; bounded
+constexpr size_t kMaxTags = 32;
+
+void tag_stats(const at::Tensor& stats, const at::Tensor& z, double T, bool mp) {
+  std::lock_guard<std::mutex> lock(g_tag_mu);
+  g_tags.erase(std::remove_if(g_tags.begin(), g_tags.end(), [](const StatsTag& t) { return t.stats.expired(); }),
+               g_tags.end());
+  if (g_tags.size() >= kMaxTags) g_tags.erase(g_tags.begin());
+  g_tags.push_back(StatsTag{c10::weak_intrusive_ptr<c10::TensorImpl>(stats.getIntrusivePtr()),
+                            c10::weak_intrusive_ptr<c10::TensorImpl>(z.getIntrusivePtr()), stats._version(),
+                            z._version(), T, mp});
+}
+
+bool stats_match(const at::Tensor& stats, const at::Tensor& z, double T, bool mp) {
+  if (!stats.defined() || !z.defined()) return false;
+  std::lock_guard<std::mutex> lock(g_tag_mu);
+  for (auto it = g_tags.rbegin(); it != g_tags.rend(); ++it) {
+    auto sp = it->stats.lock();
+    if (!sp || sp.get() != stats.unsafeGetTensorImpl()) continue;
+    auto zp = it->z.lock();
+    return zp && zp.get() == z.unsafeGetTensorImpl() && it->z_ver == z._version() &&
+           it->stats_ver == stats._version() && it->T == T && it->mp == mp;
+  }
+  return false;
+}
+}  // namespace
+
 std::vector<at::Tensor> forward_with_stats(const at::Tensor& z, double T, bool use_mixed_precision) {
   auto out = fused_forward(z.contiguous(), T, use_mixed_precision ? "fp16" : "auto", false);
   const int R = (int)z.size(0);
   auto lse_nat = out[4].narrow(0, 0, R) * (float)0.6931471805599453;
+  tag_stats(lse_nat, z, T, use_mixed_precision);
   return {out[0], lse_nat};
 }
 
 // backward(z, stats, grad_out, T): the reference passes a softmax matrix here that its own
 // forward never returns (src/ntxent_kernel.cu:202). Here `stats` may be the per-row LSE that
-// forward_with_stats returns ([2N] fp32, natural log): the backward then costs ONE similarity
+// forward_with_stats returned for this z (see StatsTag): the backward then costs ONE similarity
 // GEMM (the cosines are recomputed inside the coefficient GEMM; a stateless op keeps none).
-// Anything else in that slot (the reference's softmax, an empty tensor) is ignored and the row
-// statistics are recomputed (one more similarity GEMM), so results never depend on a stale
-// caller-provided softmax.
-// Returns (grad_z, grad_logits) where grad_logits = dL/dS is materialised only for 2N <= 4096.
+// Anything else in that slot is ignored and the row statistics are recomputed (one more
+// similarity GEMM).
+// Returns (grad_z, grad_logits). grad_logits = dL/dS [2N, 2N] (fp32) is a debug/parity output
+// built only when want_grad_logits is set; otherwise it is an empty tensor, so the default call
+// runs no extra GEMM and allocates nothing quadratic.
 std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at::Tensor& stats,
-                                               const at::Tensor& grad_out, double T, bool use_mixed_precision) {
+                                               const at::Tensor& grad_out, double T, bool use_mixed_precision,
+                                               bool want_grad_logits) {
   auto z = z_in.contiguous();
   const at::DeviceGuard guard(z.device());
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
@@ -720,7 +708,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   const long R = z.size(0), n = R / 2, Rp = P->g.rows_pad;
   at::Tensor lse2, cpos;
   const bool have_lse = stats.defined() && stats.dim() == 1 && stats.size(0) == R && stats.is_floating_point() &&
-                        stats.device() == z.device();
+                        stats.device() == z.device() && stats_match(stats, z_in, T, use_mixed_precision);
   if (have_lse) {
     // lse2 in log2 units; C_i,p(i) = -(a_i + a_p(i)), a_i = 1 - P_ip = -expm1(y_ip - lse_i)
     // (expm1 keeps a_i accurate when P_ip -> 1)
@@ -742,7 +730,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
   auto dh = norm_bwd(slabs, z, pr[1], go, *P);
   at::Tensor grad_logits;
-  if (z.size(0) <= 4096) {
+  if (want_grad_logits) {
     // dL/dS_ij = grad_out * (P_ij - [j == p(i)]) / 2N  (debug/parity output)
     auto zf = z.to(at::kFloat);
     auto zn = zf / zf.norm(2, {1}, true).clamp_min(1e-12);
@@ -772,7 +760,7 @@ bool check_tensor_core_support() {
 // ---- torch.ops registration (python/test.py:137 resolves `torch.ops.ntxent_cuda`) -------
 TORCH_LIBRARY(ntxent_cuda, m) {
   m.def("forward(Tensor z, float T, bool use_mixed_precision=False) -> Tensor");
-  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False) -> (Tensor, Tensor)");
+  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False, bool want_grad_logits=False) -> (Tensor, Tensor)");
   m.def("check_tensor_core_support() -> bool", &ntxent::th::check_tensor_core_support);
 }
 TORCH_LIBRARY_IMPL(ntxent_cuda, CUDA, m) {
@@ -782,7 +770,7 @@ TORCH_LIBRARY_IMPL(ntxent_cuda, CUDA, m) {
 TORCH_LIBRARY(ntxent, m) {
   m.def("forward(Tensor z, float T, bool use_mixed_precision=False) -> Tensor");
   m.def("forward_with_stats(Tensor z, float T, bool use_mixed_precision=False) -> Tensor[]");
-  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False) -> (Tensor, Tensor)");
+  m.def("backward(Tensor z, Tensor softmax, Tensor grad_out, float T, bool use_mixed_precision=False, bool want_grad_logits=False) -> (Tensor, Tensor)");
 }
 TORCH_LIBRARY_IMPL(ntxent, CUDA, m) {
   m.impl("forward", &ntxent::th::forward_op);
@@ -815,7 +803,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("small", &Plan::small)
-      .def_readonly("exp_bwd", &Plan::exp_bwd)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
   m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
@@ -828,17 +815,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"));
-  m.def("fwd_stats",
-        [](const at::Tensor& zl, const at::Tensor& za, const Plan& P, bool keep, bool ex) {
-          return fwd_stats(zl, za, P, keep, ex);
-        },
-        py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"), py::arg("store_exp") = false);
+  m.def("fwd_stats", &fwd_stats, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"));
   m.def("lse", &lse, py::arg("part"), py::arg("ypos"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
         py::arg("zq") = py::none(), py::arg("zqt") = py::none());
   m.def("coef", &coef);
   m.def("coef_gemm", &coef_gemm);
   m.def("dz", &dz);
-  m.def("set_exp_backward", &set_exp_backward, py::arg("on"));
   m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
   m.def("set_splitk_reduce", &ntxent::set_splitk_reduce, py::arg("on"));
   m.def("set_diag_subtiles", &ntxent::set_diag_subtiles, py::arg("on"));
@@ -846,10 +828,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
   m.def("diag_strips_enabled", &ntxent::diag_strips_enabled);
-  m.def("exp_backward_enabled", &exp_backward_enabled);
-  m.def("dz_exp", &dz_exp, py::arg("ebuf"), py::arg("zqt_all"), py::arg("lse2_all"), py::arg("plan"));
-  m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"),
-        py::arg("zq_pos") = py::none(), py::arg("cpos") = py::none());
+  m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"));
   m.def("fwd_stats_tiles", &fwd_stats_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
         py::arg("tiles"), py::arg("plan"), py::arg("part"));
   m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
@@ -868,16 +847,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);
-  m.def("set_grid_reserve", &set_grid_reserve, py::arg("cus"),
+  m.def("set_grid_reserve", &ntxent::set_grid_reserve, py::arg("cus"),
         "CUs the next similarity-GEMM launches leave free (for overlapped RCCL kernels); returns the old value");
-  m.def("set_small_path", &set_small_path, py::arg("on"));
-  m.def("small_path_enabled", &small_path_enabled);
-  m.def("set_small_splits", &set_small_splits, py::arg("n"));
+  m.def("set_small_path", &ntxent::set_small_path, py::arg("on"));
+  m.def("small_path_enabled", &ntxent::small_path_enabled);
+  m.def("set_small_splits", &ntxent::set_small_splits, py::arg("n"));
   // reference API names and kwargs
   m.def("forward", &forward_op, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
   m.def("forward_with_stats", &forward_with_stats, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
   m.def("backward", &backward_op, py::arg("z"), py::arg("softmax"), py::arg("grad_out"), py::arg("T"),
-        py::arg("use_mixed_precision") = false);
+        py::arg("use_mixed_precision") = false, py::arg("want_grad_logits") = false);
   m.def("check_tensor_core_support", &check_tensor_core_support);
   m.def("check_matrix_core_support", &check_tensor_core_support);
   m.def("get_optimal_block_size", &ntxent::get_optimal_block_size);

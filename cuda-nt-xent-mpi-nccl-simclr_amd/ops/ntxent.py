@@ -135,8 +135,11 @@ def forward_with_stats(z: torch.Tensor, T: float, use_mixed_precision: bool = Fa
 
 
 def backward(z: torch.Tensor, softmax: torch.Tensor, grad_out: torch.Tensor, T: float,
-             use_mixed_precision: bool = False):
-    return tuple(_ext.load().backward(z, softmax, grad_out, float(T), use_mixed_precision))
+             use_mixed_precision: bool = False, want_grad_logits: bool = False):
+    """(grad_z, grad_logits). `softmax` may be the LSE that forward_with_stats returned for this
+    very z (then the row statistics are not recomputed); grad_logits = dL/dS is built only when
+    want_grad_logits is set (else an empty tensor)."""
+    return tuple(_ext.load().backward(z, softmax, grad_out, float(T), use_mixed_precision, want_grad_logits))
 
 
 def check_tensor_core_support() -> bool:

@@ -24,7 +24,9 @@ def test_reference_signatures():
     assert list(sig.parameters) == ["z", "T", "use_mixed_precision"]
     assert sig.parameters["use_mixed_precision"].default is False
     sig = inspect.signature(ntxent_amd.backward)
-    assert list(sig.parameters) == ["z", "softmax", "grad_out", "T", "use_mixed_precision"]
+    # the reference's five parameters first; the opt-in debug output after them
+    assert list(sig.parameters)[:5] == ["z", "softmax", "grad_out", "T", "use_mixed_precision"]
+    assert sig.parameters["want_grad_logits"].default is False
 
 
 def test_extension_loads_and_registers_ops():
@@ -37,6 +39,7 @@ def test_extension_loads_and_registers_ops():
     assert hasattr(torch.ops.ntxent, "forward_with_stats")
     schema = str(torch.ops.ntxent_cuda.forward.default._schema)
     assert "use_mixed_precision=False" in schema
+    assert "want_grad_logits=False" in str(torch.ops.ntxent_cuda.backward.default._schema)
 
 
 def test_cpu_tensors_use_oracle_with_autograd():

@@ -148,15 +148,16 @@ def test_reference_api_forward_backward(ext):
     assert abs(loss.item() - lref.item()) < 1e-4
     assert torch.allclose(lse.double().cpu(), lse_ref, atol=1e-4)
     go = torch.tensor(1.0, device=h.device)
-    gz, glog = ext.backward(h, lse, go, 0.07)
+    gz, glog = ext.backward(h, lse, go, 0.07, want_grad_logits=True)
     gref = R.ntxent_backward_analytic(h.double().cpu(), 0.07)
     # with the caller's fp32 LSE the positive coefficient a_i = 1 - P_ip inherits the LSE's
     # rounding (~1e-6 absolute); these views are nearly saturated (P_ip -> 1, |grad| ~ 3e-6), so
     # the stats path is held to that absolute level, the recomputing path to 1e-4 relative
     assert (gz.double().cpu() - gref).abs().max() < 5e-3 * gref.abs().max() + 1e-9
     assert glog.shape == (64, 64)
-    gz2, _ = torch.ops.ntxent_cuda.backward(h, torch.empty(64, 64, device=h.device), go, 0.07)
+    gz2, glog2 = torch.ops.ntxent_cuda.backward(h, torch.empty(64, 64, device=h.device), go, 0.07)
     assert (gz2.double().cpu() - gref).abs().max() < 1e-4 * gref.abs().max() + 1e-9
+    assert glog2.numel() == 0  # grad_logits only on request
     assert torch.ops.ntxent_cuda.forward(h, 0.07).item() == pytest.approx(loss.item(), rel=1e-6)
     assert ext.check_tensor_core_support() is True
 
@@ -174,6 +175,28 @@ def test_raw_backward_with_stats_skips_forward(ext, rows, dim, mp):
     assert (g1 - g2).abs().max().item() <= (1e-5 if not mp else 2e-3) * scale
     gref = 0.5 * R.ntxent_backward_analytic(h.double().cpu(), 0.1)
     assert (g1.double().cpu() - gref).abs().max().item() <= (2e-4 if not mp else 2e-2) * gref.abs().max().item()
+
+
+def test_raw_backward_ignores_stale_stats(ext):
+    """An LSE is trusted only for the z tensor, T and precision forward_with_stats returned it
+    for: after an in-place update of z, or at another temperature, the backward recomputes the
+    statistics and matches the stateless path (stale stats gave silent errors)."""
+    _, h = _inputs(600, 200, torch.float32, seed=3)
+    _, lse = ext.forward_with_stats(h, 0.1)
+    go = torch.tensor(1.0, device=h.device)
+    # other temperature: ignored
+    g1, _ = ext.backward(h, lse, go, 0.2)
+    g2, _ = ext.backward(h, torch.empty(0, device=h.device), go, 0.2)
+    assert torch.equal(g1, g2)
+    # z changed in place after the forward: ignored
+    h.mul_(1.5).add_(0.25)
+    g3, _ = ext.backward(h, lse, go, 0.1)
+    g4, _ = ext.backward(h, torch.empty(0, device=h.device), go, 0.1)
+    assert torch.equal(g3, g4)
+    # a copy of the LSE (not the returned tensor) is not trusted either
+    _, lse2 = ext.forward_with_stats(h, 0.1)
+    g5, _ = ext.backward(h, lse2.clone(), go, 0.1)
+    assert torch.equal(g5, g4)
 
 
 @pytest.mark.parametrize("B", [16, 32, 64, 128])
