@@ -348,16 +348,23 @@ int main(int argc, char** argv) {
     else if (a == "--no-splitk") ntxent::set_splitk_reduce(false);
     else if (a == "--no-subtiles") ntxent::set_diag_subtiles(false);
     else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
+    else if (a == "--no-dzsym") ntxent::set_dz_sym(false);
+    else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
+    else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
+    else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
+    else if (a == "--small-fuse-rows") ntxent::set_small_fuse_rows(std::stoi(next()));
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
                   "                    [--recompute] [--no-small] [--gpus N] [--json out.json]\n"
                   "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n"
+                  "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
+                  "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"
                   "  --no-strips: forward remainder tiles by the stream-K split instead of diagonal strips (A/B)\n"
-                  "  --exp / --no-exp: coefficient-free backward (exponential store, C formed in the dZ GEMM) or\n"
-                  "                    the coefficient pass + dZ GEMM (default)\n");
+                  "  --no-dzsym: backward through mirrored coefficient tiles + ZqT + launch_dz (A/B against the\n"
+                  "              default upper-triangular C + Zq dZ GEMM)\n");
       return 0;
     }
   }

@@ -40,6 +40,12 @@ struct EngineConfig {
   DType compute = DType::F16;
 #endif
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
+  // dZ from the upper-triangular coefficient tiles and the gathered Zq rows (launch_dz_sym) on
+  // eligible plans: no mirrored C tiles, no ZqT transpose / gather
+  bool dz_sym = true;
+  // FP8 compute: the backward's coefficient matrix and Z^T in e4m3 too (Q8Stats; world 1).
+  // -1: the process default (set_fp8_backward), 0 / 1: off / on.
+  int fp8_backward = -1;
   bool check_finite = false;  // loss() throws on a non-finite loss
   bool small_path = true;     // single-rank small problems: the one-launch fwd / bwd kernels
   int small_splits = 0;       // small path: backward column splits (0: small_bwd_splits)
@@ -94,6 +100,14 @@ class Engine {
   int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
+  bool sym_ = false;           // launch_dz_sym backward (EngineConfig::dz_sym)
+  bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
+  float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
+  float* dot_ = nullptr;       // dot [Rpad]
+  bool q8_ = false;            // fp8 backward (e4m3 C and Z^T, EngineConfig::fp8_backward)
+  float* q8_mneg_ = nullptr;   // Q8Stats: negatives-only row max [Rpad], min LSE [1]
+  float* q8_lmin_ = nullptr;
+  char* zq8t_ = nullptr;       // e4m3(256 Zq^T) [dim_n][q8_ldt]
   bool small_ = false;        // small-problem path (small_kernels.hip)
   void* small_scratch_ = nullptr;
   DType bwd_ = DType::F16;

@@ -226,9 +226,27 @@ int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
 int lse_scratch_floats(const Geometry& g);
 // zq / zqt (optional, rank-local [Rpad, ld_k] rows in tr_dtype): the same launch also writes the
 // transpose zqt = zq^T (launch_transpose) from extra blocks that run beside the merge.
+//
+// fp8 backward (FP8 plans, set_fp8_backward; world 1, kept cosines): the coefficient matrix and
+// Z^T go to the dZ GEMM as e4m3. C row i is scaled by 2^q8_row_exp(mneg2_i, lmin) (a bound on
+// its negatives from the LSE pass; the positive C_ip is excluded and added exactly in the dZ
+// epilogue), Z^T by 256. Q8Stats carries the LSE pass's extra outputs: mneg2 [Rpad] (each row's
+// negatives-only max logit, log2 units), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
+// bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
+void set_fp8_backward(bool on);  // default: see ntxent_kernels.hip
+bool fp8_backward_enabled();
+bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
+int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad
+struct Q8Stats {
+  float* mneg2 = nullptr;
+  float* lmin = nullptr;
+  void* zq8t = nullptr;
+  const void* zq = nullptr;  // fp16 rows (the dZ epilogue's positive term C_ip z_p)
+};
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos,
                 float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream,
-                DType tr_dtype = DType::F16, const void* zq = nullptr, void* zqt = nullptr);
+                DType tr_dtype = DType::F16, const void* zq = nullptr, void* zqt = nullptr,
+                const Q8Stats* q8 = nullptr);
 
 // Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
 // `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;
@@ -237,22 +255,62 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 // tiles with slot = (q - rank - 1) mod W (partners rank+1, rank+2, ... in order): tile (mt, nt)
 // lands transposed at mbuf tile (slot, nt % row_tiles, mt), i.e. the block C_{q,rank} that
 // multiplies this rank's rows in rank q's gradient; consecutive slots stack into one tall A.
+// upper_only: write only the tiles of `tiles` themselves (no mirrored lower own-block tiles): the
+// layout launch_dz_sym reads.
+// dotp (optional, [Rpad][dot_slots(g)] floats): partials of dot_i = sum_j C_ij cos_ij, the
+// z_i . g_i of the normalisation backward, for the fused dZ epilogue (NormFuse); every slot is
+// written (all-gather layout, own-block tiles + remote tiles of the plan).
+int dot_slots(const Geometry& g);
+// q8 (fp8 backward): cbuf receives e4m3 tiles (1 byte per element, same tile layout, mirrored
+// own-block tiles written: launch_dz reads them), scaled per row as Q8Stats says; dotp then holds
+// the partials of the dequantised coefficients (plus the exact positive term).
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf = nullptr);
+                 void* mbuf = nullptr, bool upper_only = false, float* dotp = nullptr,
+                 const Q8Stats* q8 = nullptr);
+// dot[Rpad] = row sums of dotp.
+void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream);
 
 // Recompute variant (no stored cosines): GEMM S tiles again and emit C tiles into `cbuf`.
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
-                      const BlockView& bv = BlockView{});
+                      const BlockView& bv = BlockView{}, float* dotp = nullptr);
 
 // dZ[Rpad][dim_n] = C * Z (fp32), C = the coefficient buffer, zqt_all = [W][dim_n][Rpad]
 // (all-gathered ZqT blocks); tiles from build_dz_tiles(g).
 // out_f16: write dZ as fp16 (the reduced-precision plans: half the bytes of the dZ store and of
 // the normalisation backward's read; |dZ| <= ~4, fp16 keeps 11 bits against the bf16/fp16 dh).
-void launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
-               void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false);
+// Fused normalisation backward of the dZ GEMM's epilogue: dh = grad_out/(2N tau) inv (g - z dot)
+// computed per tile from the fp16-staged g, h, inv and dot (launch_dot_reduce); the dZ slab is
+// not written. The launchers return whether they fused (not for split-K dZ pieces or d % 8 != 0:
+// then the slab is written and launch_norm_bwd runs as before).
+void set_norm_fuse(bool on);  // default on; off = dZ slab + launch_norm_bwd (A/B)
+bool norm_fuse_enabled();
+struct NormFuse {
+  const void* h = nullptr;
+  DType in = DType::BF16;
+  const float* inv = nullptr;
+  const float* dot = nullptr;
+  const float* grad_out = nullptr;  // device scalar
+  void* dh = nullptr;
+};
+// comp = FP8 with q8: the fp8 backward's dZ (cbuf = e4m3 C tiles, zqt_all = Q8Stats::zq8t;
+// block-scaled MFMA, per-row dequantisation and the exact positive term in the epilogue).
+bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
+               void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false,
+               const NormFuse* nf = nullptr, const Q8Stats* q8 = nullptr, const float* cpos = nullptr);
+
+// dZ = C * Zq (all-gather layout) from the coefficient tiles launch_coef(..., upper_only) wrote
+// (own-block upper triangle + remote tiles; a lower own tile is read as the transpose of the
+// stored one) and the normalised rows zq_all [W * Rpad][ld_k] themselves (no ZqT): 64 MiB less
+// coefficient store and no transpose at the headline. Plans: dz_sym_eligible.
+bool dz_sym_eligible(const Geometry& g, DType comp);
+void set_dz_sym(bool on);  // default on; off = coefficient mirrors + ZqT + launch_dz (A/B)
+bool dz_sym_enabled();
+bool launch_dz_sym(DType comp, const void* cbuf, const void* zq_all, const int4* tiles, int ntiles, void* dz,
+                   const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = true,
+                   const NormFuse* nf = nullptr);
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first
@@ -273,9 +331,9 @@ void launch_norm_bwd(DType in, const float* slabs, int nslabs, const void* h,
                      hipStream_t stream, const void* xslabs = nullptr, int nx = 0);
 
 // ---- small-problem path (kernels/small_kernels.hip) -------------------------------------
-// Single-rank problems with R <= kSmallMaxRows and dim_k <= kSmallMaxDk in fp16/bf16: after
-// launch_prep, ONE forward launch (64 x 64 MFMA tiles, in-kernel LSE merge and deterministic
-// loss sum) and ONE backward launch (S recomputed, C formed in registers and fed straight to
+// Single-rank problems with R <= kSmallMaxRows and dim_k <= kSmallMaxDk in fp16/bf16: ONE
+// forward launch (row prologue fused for R <= kSmallFuseMaxRows, else after launch_prep; 64 x 64
+// MFMA tiles, in-kernel LSE merge and deterministic loss sum) and ONE backward launch (S recomputed, C formed in registers and fed straight to
 // the dZ MFMA, normalisation backward fused). `scratch` (small_scratch_bytes) must be ZERO when
 // first used (its arrival counters return to zero after every launch); launches sharing it must
 // be stream-ordered. lse2 / arow ([small_rows_pad(g)] floats) carry the row statistics from the
@@ -286,8 +344,15 @@ bool small_path_eligible(const Geometry& g, DType comp);
 int small_bwd_splits(const Geometry& g);  // default column splits of the backward grid
 int small_rows_pad(const Geometry& g);    // roundup(R, 64)
 size_t small_scratch_bytes(const Geometry& g, int splits);
-void launch_small_fwd(DType comp, const void* zq, const float* ypos, float* lse2, float* arow, float* loss,
-                      void* scratch, const Geometry& g, hipStream_t stream);
+constexpr int kSmallFuseMaxRows = 1024;  // measured: see profiles/r3/small/
+bool small_fwd_fused(const Geometry& g);  // the forward runs the row prologue itself
+void set_small_fuse_rows(int rows);       // override kSmallFuseMaxRows (-1: default)
+int small_fuse_rows_override();
+// h: [R][dim] input (dtype `in`). Writes zq ([small_rows_pad][ld_k], compute dtype, pad rows zero)
+// and inv ([R]) when small_fwd_fused(g); otherwise zq / inv / ypos are launch_prep's outputs
+// (ypos ignored when fused).
+void launch_small_fwd(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos, float* lse2,
+                      float* arow, float* loss, void* scratch, const Geometry& g, hipStream_t stream);
 // splits <= 0: small_bwd_splits(g). grad_out: device fp32 scalar.
 void launch_small_bwd(DType in, DType comp, const void* zq, const void* h, const float* inv, const float* lse2,
                       const float* arow, const float* grad_out, void* dh, void* scratch, const Geometry& g,

@@ -21,6 +21,7 @@ constexpr int kNumXcdDev = 8;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 constexpr float kNegInf = -__builtin_huge_valf();
+constexpr float kPosInf = __builtin_huge_valf();
 
 // ---- dtype conversion --------------------------------------------------------------
 template <typename T> __device__ __forceinline__ float to_f32(T x);
@@ -144,6 +145,18 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
   s = s * fast_exp2(m - mn) + s2 * fast_exp2(m2 - mn);
   m = mn;
 }
+
+// fp8 backward: power-of-two scale 2^e of row i's coefficients in the e4m3 C matrix. Every
+// negative coefficient C_ij = P_ij + P_ji is at most 2^(m_i - lse_i) + 2^(m_i - L) <= 2 * 2^(m_i - L)
+// (m_i: row i's largest negative logit, L: the smallest LSE of any row, log2 units; y_ij = y_ji
+// <= m_i), so C_ij * 2^e <= 448 (e4m3 max) with e = floor(log2(448 / 2) - (m_i - L)). The positive
+// coefficient is not stored in e4m3 (the dZ epilogue adds C_ip z_p exactly). Empty / padded rows
+// (m_i = -inf) and extreme rows are clamped.
+__device__ __forceinline__ int q8_row_exp(float mneg2, float lmin) {
+  const float e = floorf(7.807f - (mneg2 - lmin));
+  return (int)fminf(fmaxf(e, -60.f), 60.f);
+}
+__device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }  // |e| <= 126
 
 // Block-wide sum for up to 1024 threads; `red` must hold >= 16 floats. All threads get it.
 __device__ __forceinline__ float block_sum(float x, float* red) {

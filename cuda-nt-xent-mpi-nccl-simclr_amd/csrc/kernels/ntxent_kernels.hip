@@ -15,6 +15,7 @@
 #include "../include/ntxent/ntxent.h"
 #include "device_common.h"
 #include "sim_gemm.h"
+#include "dz_sym.h"
 
 #include <atomic>
 #include <algorithm>
@@ -386,6 +387,35 @@ __device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __re
   }
 }
 
+// fp8 backward operand: e4m3(256 Z^T) ([dim_n][ldt] bytes) from the fp16 rows, same tiling (the
+// gathered 8 elements go out as one 8-byte store). |z| <= 1, so 256 z stays below the e4m3 max.
+__device__ __forceinline__ void transpose_tile_q8(const _Float16* __restrict__ zq, unsigned char* __restrict__ zqt,
+                                                  int dk, int ldk, int ldt, int bx, int by, _Float16 (&tile)[64][72]) {
+  constexpr int V = 8, CPR = 8;
+  const int j0 = bx * 64, e0 = by * 64;
+  for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
+    const int r = k / CPR, c = k % CPR;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * ldk + e0 + c * V);
+    *reinterpret_cast<u32x4*>(&tile[r][(c ^ ((r / V) % CPR)) * V]) = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
+    const int er = k / CPR, jc = k % CPR;
+    float x[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) x[q] = 256.f * (float)tile[jc * V + q][((er / V) ^ (jc % CPR)) * V + er % V];
+    u32x2 o;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h], x[4 * h + 1], 0, false);
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(x[4 * h + 2], x[4 * h + 3], w, true);
+      o[h] = (unsigned)w;
+    }
+    *reinterpret_cast<u32x2*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = o;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
                                                         int dk, int ldk, int ldt) {
@@ -420,6 +450,10 @@ struct LseArgs {
   float* loss_sum;
   float loss_scale;
   int R, Rpad, Tc, own0;
+  // fp8 backward (q8_row_exp): each row's negatives-only max logit and the global min LSE (log2
+  // units); null otherwise
+  float* mneg2;
+  float* lmin;
 };
 // Block `bid` of the nb LSE blocks (the last of them to finish sums the loss).
 __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, float* red, int& last) {
@@ -430,7 +464,7 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
   const int n = R >> 1;
   const int gt = bid * 256 + threadIdx.x;
   const int item = gt / kLseLanes, q = gt % kLseLanes;
-  float li = 0.f;
+  float li = 0.f, lmn = kPosInf;
   if (item < n) {  // uniform across the 8 lanes of an item
     const int i = item, j = item + n;
     float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
@@ -460,18 +494,23 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
     if (q == 0) {
       const float yp = a.ypos[i];
       float l_i, l_j, a_i, a_j;
-      lse2_all[own0 + i] = finish_row(mi, si, yp, l_i, a_i);
-      lse2_all[own0 + j] = finish_row(mj, sj, yp, l_j, a_j);
+      const float L2i = finish_row(mi, si, yp, l_i, a_i), L2j = finish_row(mj, sj, yp, l_j, a_j);
+      lse2_all[own0 + i] = L2i;
+      lse2_all[own0 + j] = L2j;
       cpos[i] = -(a_i + a_j);
       cpos[j] = -(a_i + a_j);
       li = l_i + l_j;
+      lmn = fminf(L2i, L2j);
+      if (a.mneg2) { a.mneg2[own0 + i] = mi; a.mneg2[own0 + j] = mj; }
     }
   } else if (item < Rpad - n && q == 0) {
     const int i = R + (item - n);
     lse2_all[own0 + i] = 0.f;
     cpos[i] = 0.f;
+    if (a.mneg2) a.mneg2[own0 + i] = kNegInf;
   }
   const float tot = block_sum(li, red);
+  const float bmin = a.lmin ? -block_max(-lmn, red) : 0.f;
   // Last-block-done final sum (replaces a separate one-thread launch): publish this block's
   // partial, count arrivals; the last block adds all partials in block order (deterministic)
   // and returns the counter (a fixed slot ahead of the partials) to zero. The partial is a
@@ -480,8 +519,10 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
   // row 1); a release fence here wrote back every dirty L2 line the forward GEMM left behind.
   int* cnt = reinterpret_cast<int*>(a.block_loss);  // fixed slot 0: the counter
   float* partial = a.block_loss + 64;               // per-block partials after it
+  float* pmin = partial + nb;                       // per-block LSE minima (fp8 backward)
   if (threadIdx.x == 0) {
     __hip_atomic_store(partial + bid, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.lmin) __hip_atomic_store(pmin + bid, bmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == nb - 1;
@@ -494,6 +535,13 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
       s += __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s = wave_sum(s);  // fixed lane assignment and tree: deterministic
     if (threadIdx.x == 0) a.loss_sum[0] = s * a.loss_scale;
+    if (a.lmin) {
+      float m = kPosInf;
+      for (int b = threadIdx.x; b < nb; b += 64)
+        m = fminf(m, __hip_atomic_load(pmin + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      m = -xrow_max(row16_max(-m));
+      if (threadIdx.x == 0) a.lmin[0] = m;
+    }
   }
 }
 
@@ -507,9 +555,10 @@ __global__ __launch_bounds__(256) void lse_kernel(const LseArgs a) {
 // [0, nb) merge, the rest transpose one 64x64 tile each. The merge is latency-bound on few
 // blocks and the transpose is bandwidth-bound on many, so they share the chip instead of
 // running back to back, and no side stream / event join (a ~5-7 us bubble each) is needed.
-template <typename T>
+// Q8: the transpose writes the fp8 backward's e4m3(256 Z^T) (T = _Float16 rows in).
+template <typename T, bool Q8 = false>
 __global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int nb, const T* __restrict__ zq,
-                                                            T* __restrict__ zqt, int dk, int ldk, int ldt, int tx) {
+                                                            void* __restrict__ zqt, int dk, int ldk, int ldt, int tx) {
   __shared__ __attribute__((aligned(16))) T tile[64][64 + 16 / sizeof(T)];
   __shared__ float red[16];
   __shared__ int last;
@@ -517,7 +566,10 @@ __global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int
     lse_block(a, blockIdx.x, nb, red, last);
   } else {
     const int t = blockIdx.x - nb;
-    transpose_tile<T>(zq, zqt, dk, ldk, ldt, t % tx, t / tx, tile);
+    if constexpr (Q8)
+      transpose_tile_q8(zq, static_cast<unsigned char*>(zqt), dk, ldk, ldt, t % tx, t / tx, tile);
+    else
+      transpose_tile<T>(zq, static_cast<T*>(zqt), dk, ldk, ldt, t % tx, t / tx, tile);
   }
 }
 
@@ -610,6 +662,22 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
     const float z = to_f32<Tin>(hi[e]) * iv;
     di[e] = from_f32<Tin>(alpha * iv * (g - z * dot));
   }
+}
+
+// dot_i = sum over the coefficient pass's slots of dotp[i][.] (fixed order: deterministic).
+__global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict__ dotp, int nslot, int rows,
+                                                         float* __restrict__ dot) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows) return;
+  const float* r = dotp + (long long)i * nslot;
+  float s = 0.f;
+  int k = 0;
+  for (; k + 4 <= nslot; k += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
+    s += (v[0] + v[1]) + (v[2] + v[3]);
+  }
+  for (; k < nslot; ++k) s += r[k];
+  dot[i] = s;
 }
 
 }  // namespace dev
@@ -940,7 +1008,11 @@ static std::atomic<bool> g_coef_perm{true};      // coefficient pass: lane-permu
 static std::atomic<bool> g_splitk_reduce{true};  // split-K forward / dZ for tile-starved launches
 static std::atomic<bool> g_small_path{true};     // one-launch small-problem forward / backward
 static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
+static std::atomic<int> g_small_fuse_rows{-1};   // small forward: fused row prologue up to R rows (-1: default)
 static std::atomic<int> g_grid_reserve{0};       // CUs the GEMMs leave free for overlapped RCCL kernels
+static std::atomic<bool> g_dz_sym{true};         // dZ from the upper-triangular C and Zq (launch_dz_sym)
+static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
+static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -952,8 +1024,18 @@ void set_small_path(bool on) { g_small_path = on; }
 bool small_path_enabled() { return g_small_path.load(); }
 void set_small_splits(int n) { g_small_splits = std::max(0, n); }
 int small_splits_override() { return g_small_splits.load(); }
+void set_small_fuse_rows(int rows) { g_small_fuse_rows = rows < 0 ? -1 : rows; }
+int small_fuse_rows_override() { return g_small_fuse_rows.load(); }
 int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
 int grid_reserve() { return g_grid_reserve.load(); }
+void set_dz_sym(bool on) { g_dz_sym = on; }
+bool dz_sym_enabled() { return g_dz_sym.load(); }
+void set_fp8_backward(bool on) { g_fp8_bwd = on; }
+bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
+bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
+int q8_ldt(const Geometry& g) { return g.rows_pad; }
+void set_norm_fuse(bool on) { g_norm_fuse = on; }
+bool norm_fuse_enabled() { return g_norm_fuse.load(); }
 
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
@@ -1055,7 +1137,8 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
 
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,
                       const float* lse2_all, const float* cpos, const int4* tiles, int ntiles,
-                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, const BlockView& bv) {
+                      const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, const BlockView& bv,
+                      float* dotp) {
   if (ntiles == 0) return;
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
@@ -1069,6 +1152,7 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
   p.cbuf = static_cast<char*>(cbuf);
   p.lse2 = lse2_all;
   p.cpos = cpos;
+  p.dotp = dotp;
   p.b_tile0 = bv.b_tile0;
   if (bv.c_ld > 0) p.c_ld = bv.c_ld;
   p.c_tile0 = bv.c_tile0;
@@ -1082,22 +1166,32 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 
 static int lse_blocks(const Geometry& g) { return ((g.rows_pad - g.rows / 2) * dev::kLseLanes + 255) / 256; }
 
-int lse_scratch_floats(const Geometry& g) { return 64 + lse_blocks(g); }  // counter slot + partials
+int lse_scratch_floats(const Geometry& g) { return 64 + 2 * lse_blocks(g); }  // counter slot + partials (sum, min)
 
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
-                float* loss_sum, const Geometry& g, hipStream_t stream, DType tr_dtype, const void* zq, void* zqt) {
+                float* loss_sum, const Geometry& g, hipStream_t stream, DType tr_dtype, const void* zq, void* zqt,
+                const Q8Stats* q8) {
   const int nb = lse_blocks(g);  // one workgroup per 32 pairs / pad rows
   dev::LseArgs a{part, ypos, lse2_all, cpos, block_loss, loss_sum, (float)(1.0 / (double)g.global_rows),
                  g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad};
+  if (q8) {
+    a.mneg2 = q8->mneg2;
+    a.lmin = q8->lmin;
+  }
   if (zq == nullptr) {
     hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, a);
+  } else if (q8 && q8->zq8t) {
+    NTXENT_CHECK(tr_dtype == DType::F16 && g.world == 1, "lse: the fp8 backward transposes fp16 rows (world 1)");
+    const int tx = g.rows_pad / 64, ty = g.dim_n / 64;
+    hipLaunchKernelGGL((dev::lse_transpose_kernel<_Float16, true>), dim3(nb + tx * ty), dim3(256), 0, stream, a, nb,
+                       static_cast<const _Float16*>(zq), q8->zq8t, g.dim_k, g.ld_k, q8_ldt(g), tx);
   } else {
     NTXENT_CHECK(zqt != nullptr, "lse: transpose output missing");
     const int tx = g.rows_pad / 64, ty = g.dim_n / 64;
     dispatch_comp(tr_dtype, [&](auto tc) {
       using Tc = decltype(tc);
       hipLaunchKernelGGL((dev::lse_transpose_kernel<Tc>), dim3(nb + tx * ty), dim3(256), 0, stream, a, nb,
-                         static_cast<const Tc*>(zq), static_cast<Tc*>(zqt), g.dim_k, g.ld_k, g.ld_t, tx);
+                         static_cast<const Tc*>(zq), zqt, g.dim_k, g.ld_k, g.ld_t, tx);
     });
   }
   NTXENT_HIP_CHECK(hipGetLastError());
@@ -1105,15 +1199,26 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf) {
+                 void* mbuf, bool upper_only, float* dotp, const Q8Stats* q8) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
+  p.no_mirror = upper_only ? 1 : 0;
+  p.dotp = dotp;
   p.tiles = tiles;
   p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
   p.cbuf = static_cast<char*>(cbuf);
   p.mbuf = static_cast<char*>(mbuf);
   p.lse2 = lse2_all;
   p.cpos = cpos;
+  if (q8) {
+    NTXENT_CHECK(comp == DType::F16 && mbuf == nullptr && !upper_only && g.world == 1,
+                 "coef (fp8 backward): fp16 kept cosines, world 1, mirrored layout");
+    p.q8_mneg = q8->mneg2;
+    p.q8_lmin = q8->lmin;
+    hipLaunchKernelGGL((dev::coef_kernel<_Float16, true, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
+    NTXENT_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
     if (coef_lane_permute()) hipLaunchKernelGGL((dev::coef_kernel<Tc, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
@@ -1122,11 +1227,47 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
-               void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16) {
-  if (ntiles == 0) return;
+int dot_slots(const Geometry& g) { return 4 * g.col_tiles; }
+
+void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream) {
+  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 255) / 256), dim3(256), 0, stream, dotp, dot_slots(g),
+                     g.rows_pad, dot);
+  NTXENT_HIP_CHECK(hipGetLastError());
+}
+
+// Fused normalisation backward in the dZ epilogue (dz_store), or for split-K pieces in the reduce
+// launch (sk_dz_reduce_kernel): rows must be whole 16-byte chunks.
+static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometry& g) {
+  if (nf == nullptr || nf->dh == nullptr || g.dim % 8 != 0) return false;
+  p.nh = nf->h;
+  p.nh_dt = nf->in == DType::F32 ? 0 : (nf->in == DType::F16 ? 1 : 2);
+  p.nd = g.dim;
+  p.ninv = nf->inv;
+  p.ndot = nf->dot;
+  p.ngo = nf->grad_out;
+  p.nalpha = (float)(1.0 / ((double)g.global_rows * g.temperature));
+  p.ndh = nf->dh;
+  p.out_f16 = 1;
+  p.accum = 0;
+  return true;
+}
+
+bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
+               void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
+               const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
+  if (ntiles == 0) return false;
+  const bool f8 = comp == DType::FP8;
+  NTXENT_CHECK(!f8 || (q8 && q8->mneg2 && q8->lmin && q8->zq && cpos && g.world == 1 && out_f16),
+               "dz (fp8 backward): Q8Stats, cpos, world 1 and an fp16 slab required");
   const long long cs = (long long)dtype_size(comp);
   dev::SimParams p = base_params(g);
+  if (f8) {
+    p.q8_mneg = q8->mneg2;
+    p.q8_lmin = q8->lmin;
+    p.q8_zq = static_cast<const _Float16*>(q8->zq);
+    p.q8_ldz = g.ld_k;
+    p.cpos = cpos;
+  }
   // A = C, tile-blocked: rows of a 256x256 tile are 256 elements; every 256 K-columns jump
   // to the next tile of the row panel.
   p.A.base = static_cast<const char*>(sc);
@@ -1136,10 +1277,11 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.A.kblk_stride = kTileElems * cs;
   // B = ZqT_all [W][dim_n][ld_t]: rows = embedding dims, K = global columns, one K block per rank.
   p.B.base = static_cast<const char*>(zqt_all);
-  p.B.ld = (long long)g.ld_t * cs;
-  p.B.row_tile_stride = (long long)kTile * g.ld_t * cs;
+  const long long ldt = f8 ? q8_ldt(g) : g.ld_t;
+  p.B.ld = ldt * cs;
+  p.B.row_tile_stride = (long long)kTile * ldt * cs;
   p.B.kblk = (long long)g.rows_pad * cs;
-  p.B.kblk_stride = (long long)g.dim_n * g.ld_t * cs;
+  p.B.kblk_stride = (long long)g.dim_n * ldt * cs;
   p.tiles = tiles;
   p.kbytes = (long long)g.world * g.rows_pad * cs;
   p.out = static_cast<float*>(slabs);
@@ -1151,7 +1293,8 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
   const int nk = (int)(p.kbytes / kKStepBytes);
   int pieces = fwd_splitk_pieces(ntiles, nk, cus, 1);
-  if (pieces < 3) pieces = 0;  // 2 pieces: the reduce launch costs more than the fixup it replaces
+  if (pieces < 3 || f8) pieces = 0;  // 2 pieces: the reduce launch costs more than the fixup it replaces
+  // (fp8: the finishing block's dequantisation lives in the GEMM epilogue, not the reduce)
   int grid;
   if (pieces > 0) {
     p.nk = nk;
@@ -1168,12 +1311,66 @@ void launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   } else {
     grid = apply_schedule(p, ntiles, ws, stream);
   }
-  dispatch_comp(comp, [&](auto tc) {
+  const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
+  dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
   });
   if (pieces > 0) hipLaunchKernelGGL(dev::sk_dz_reduce_kernel, dim3(ntiles * 64), dim3(256), 0, stream, p);
   NTXENT_HIP_CHECK(hipGetLastError());
+  return fused;
+}
+
+bool dz_sym_eligible(const Geometry& g, DType comp) {
+  // 16-bit operands (transposed LDS reads) and Zq rows that hold every column of a d-tile
+  // (dim_k == dim_n: the B half-tiles never read past a row)
+  return (comp == DType::F16 || comp == DType::BF16 || comp == DType::FP8) && g.dim_k == g.dim_n;
+}
+
+bool launch_dz_sym(DType comp, const void* cbuf, const void* zq_all, const int4* tiles, int ntiles, void* slabs,
+                   const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16, const NormFuse* nf) {
+  if (ntiles == 0) return false;
+  const DType bc = backward_dtype(comp);
+  NTXENT_CHECK(dz_sym_eligible(g, comp), "dz_sym: plan not eligible (16-bit backward dtype, dim_k == dim_n)");
+  const long long cs = 2;
+  dev::SimParams p = base_params(g);
+  p.A.base = static_cast<const char*>(cbuf);  // tiles [row_tiles][col_tiles], upper own block stored
+  if (std::getenv("NTXENT_DZSYM_NOMIR")) p.row_tile0 = 1 << 20;  // DIAGNOSTIC: full C, no mirrored steps
+  p.B.base = static_cast<const char*>(zq_all);
+  p.B.ld = (long long)g.ld_k * cs;
+  p.tiles = tiles;
+  p.kbytes = (long long)g.world * g.rows_pad * cs;
+  p.out = static_cast<float*>(slabs);
+  p.out_f16 = out_f16 ? 1 : 0;
+  p.ldo = g.dim_n;
+  p.slab_stride = (long long)g.rows_pad * g.dim_n;
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  int pieces = fwd_splitk_pieces(ntiles, nk, cus, 1);
+  if (pieces < 3) pieces = 0;
+  int grid;
+  if (pieces > 0) {
+    p.nk = nk;
+    p.dp_tiles = 0;
+    p.sk_tiles = ntiles;
+    p.ipb = (nk + pieces - 1) / pieces;
+    p.sk_out = 1;
+    p.sk_cnt = static_cast<int*>(ws.ptr);
+    p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+    grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
+    NTXENT_CHECK(grid <= ws.num_cus && ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
+                 "split-K dZ: workspace too small");
+  } else {
+    grid = apply_schedule(p, ntiles, ws, stream);
+  }
+  const bool fused = apply_norm_fuse(p, nf, g);
+  if (bc == DType::BF16)
+    hipLaunchKernelGGL((dev::dz_sym_kernel<__bf16>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
+  else
+    hipLaunchKernelGGL((dev::dz_sym_kernel<_Float16>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
+  if (pieces > 0) hipLaunchKernelGGL(dev::sk_dz_reduce_kernel, dim3(ntiles * 64), dim3(256), 0, stream, p);
+  NTXENT_HIP_CHECK(hipGetLastError());
+  return fused;
 }
 
 void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const void* b, long long b_kblk_cols,

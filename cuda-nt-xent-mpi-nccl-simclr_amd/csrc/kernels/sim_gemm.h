@@ -71,6 +71,23 @@ struct SimParams {
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
+  int no_mirror;         // coefficient pass: write only the stored (upper) own-block tiles (dz_sym_kernel
+                         // reads the lower ones transposed)
+  // Fused normalisation backward (see dot_slots / dz_store):
+  float* dotp;           // coefficient pass: partials of dot_i = sum_j C_ij cos_ij, [Rpad][4 col_tiles]
+  const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
+  int nh_dt, nd;
+  const float* ninv;     // ... 1 / |h_i|
+  const float* ndot;     // ... dot_i (reduced dotp)
+  const float* ngo;      // ... grad_out (device scalar)
+  float nalpha;          // ... 1 / (2N tau)
+  void* ndh;             // ... output dh [R][nd] (non-null: fused epilogue)
+  // fp8 backward (Q8Stats): per-row e4m3 scale inputs (q8_row_exp) and the fp16 rows for the
+  // dZ epilogue's exact positive term
+  const float* q8_mneg;
+  const float* q8_lmin;
+  const _Float16* q8_zq;
+  int q8_ldz;
   // persistent stream-K schedule (see sim_gemm_kernel)
   int nk;                // K-steps per tile
   int dp_tiles;          // whole-tile items processed in rounds of gridDim
@@ -141,13 +158,18 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
   T* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
   T* mirror = nullptr;
-  if (kind == kTileSymOff)
+  if (kind == kTileSymOff && !p.no_mirror)
     mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
   else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
     const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
     const int slot = (q - p.row_tile0 / rt - 1 + W) % W;  // partners r+1, r+2, ... -> slots 0, 1, ...
     mirror = reinterpret_cast<T*>(p.mbuf) + ((long long)(slot * rt + nt % rt) * rt + mt) * kTileElems;
   }
+  // dot partial slots of row i: 4 per column tile J (the quarter of J's columns a wave covered, or
+  // for the column partials of a mirrored tile the quarter of its rows); each written once
+  const int nslot = 4 * p.col_tiles;
+  const int wq = NW == 8 ? ((threadIdx.x >> 6) & 3) : (col_base >> 6);  // column quarter of this wave
+  float cdot[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
@@ -171,6 +193,25 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         c[ni][r] = v;
       }
     }
+    if (p.dotp) {
+      // dot_i = sum_j C_ij cos_ij (= z_i . g_i of the normalisation backward), with C as the dZ
+      // GEMM reads it (rounded to T): row partials over this wave's columns; for a mirrored tile
+      // also column partials (the lower tile's rows) over this wave's rows.
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float d = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) d += to_f32<T>(from_f32<T>(c[ni][r])) * acc[mi][ni][r];
+        d = row16_sum(d);
+        const int row = mt * kTile + rb[mi] + 4 * (lane >> 4) + r;
+        if ((lane & 15) == 0) p.dotp[(long long)row * nslot + nt * 4 + wq] = d;
+      }
+      const int h2 = NMI == 8 ? (mi >> 2) : 0;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cdot[h2][ni] += to_f32<T>(from_f32<T>(c[ni][r])) * acc[mi][ni][r];
+    }
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int col_t = cb[ni] + (lane & 15);
@@ -187,6 +228,20 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         if (mirror)
           *reinterpret_cast<f32x4*>(mirror + col_t * kTile + row_t0) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
       }
+    }
+  }
+  if (p.dotp) {
+    if (kind == kTileSymOff) {
+      const int wa8 = (threadIdx.x >> 6) >> 2;
+#pragma unroll
+      for (int h2 = 0; h2 < (NMI == 8 ? 2 : 1); ++h2)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const float d = xrow_sum(cdot[h2][ni]);
+          const int rq = NMI == 8 ? 2 * h2 + wa8 : (row_base >> 6);  // row quarter of this wave's rows
+          const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
+          if (lane < 16) p.dotp[(long long)row * nslot + (p.row_tile0 + mt) * 4 + rq] = d;
+        }
     }
   }
   if constexpr (sizeof(T) == 2) {
@@ -242,12 +297,406 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
 }
 
+// fp8 backward coefficient epilogue (store mode, one wave per 64 x 64 region of a kept cosine
+// tile): C as coef_epilogue, quantised to e4m3 with the row scale 2^e_i (q8_row_exp) for the
+// stored tile and 2^e_j for its mirror (row j of the lower tile); the positive entry is stored as
+// 0 (the dZ epilogue adds C_ip z_p exactly). Both byte tiles are staged in LDS (stride 80 B: the
+// column-major writes hit distinct banks) and leave as 16-byte row segments. A lane's 4 rows of
+// one column pack into a dword (the mirror's layout); for the stored tile a quad of lanes swaps
+// bytes by DPP so that each lane holds 4 consecutive columns of one row.
+__device__ __forceinline__ unsigned q8_pack4(const float (&x)[4], float sc) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(x[0] * sc, -448.f), 448.f),
+                                          fminf(fmaxf(x[1] * sc, -448.f), 448.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(x[2] * sc, -448.f), 448.f), fminf(fmaxf(x[3] * sc, -448.f), 448.f),
+                                      w, true);
+  return (unsigned)w;
+}
+__device__ __forceinline__ float q8_byte(unsigned w, int b) { return __builtin_amdgcn_cvt_f32_fp8((int)(w >> (8 * b)), 0); }
+
+template <typename TS>
+__device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (&rb)[4], const int (&cb)[4],
+                                                 int row_base, int col_base, int mt, int nt, int kind, lds_char* lds,
+                                                 const SimParams& p, int lane) {
+  constexpr int S8 = 80;  // LDS row stride of both staged byte tiles (64 B + 16 B)
+  lds_char* ld_d = lds;             // stored tile: [64 rows][64 cols]
+  lds_char* ld_m = lds + 64 * S8;   // mirror: [64 cols][64 rows]
+  unsigned char* base = reinterpret_cast<unsigned char*>(p.cbuf);
+  unsigned char* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
+  unsigned char* mirror = kind == kTileSymOff
+                              ? base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems
+                              : nullptr;
+  const int col_local0 = (nt * kTile) % p.Rpad;
+  const bool fixed = p.fixed_shift != 0;
+  const float M = p.y_scale;
+  const float lmin = p.q8_lmin[0];
+  float lcol[4], scol[4], icol[4];
+  bool cvalid[4];
+  int gj[4];
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int col_t = cb[ni] + (lane & 15);
+    gj[ni] = nt * kTile + col_t;
+    const float l = p.lse2[gj[ni]];
+    lcol[ni] = fixed ? fast_exp2(M - l) : l;
+    cvalid[ni] = (col_local0 + col_t) < p.R;
+    const int e = q8_row_exp(p.q8_mneg[gj[ni]], lmin);
+    scol[ni] = exp2i(e);
+    icol[ni] = exp2i(-e);
+  }
+  const int nslot = 4 * p.col_tiles;
+  const int wq = col_base >> 6;
+  float cdot[4] = {0.f, 0.f, 0.f, 0.f};
+  const int qd = lane & 3;  // the row of a 4-row group this lane stores after the quad swap
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int row_t0 = rb[mi] + 4 * (lane >> 4);
+    const int gi0 = mt * kTile + row_t0;
+    const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
+    const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
+    const f32x4 mneg4 = *reinterpret_cast<const f32x4*>(p.q8_mneg + p.own0 + gi0);
+    float srow[4], irow[4], rdot[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = q8_row_exp(mneg4[r], lmin);
+      srow[r] = exp2i(e);
+      irow[r] = exp2i(-e);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      float c[4];
+      bool pos[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = gi0 + r;
+        const bool rvalid = gi < p.R;
+        const float lrow = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
+        const int gself = p.own0 + gi;
+        const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
+        const float y = acc[mi][ni][r] * p.acc_scale;
+        float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
+        const bool ok = rvalid && cvalid[ni] && gj[ni] != gself;
+        pos[r] = ok && gj[ni] == gpos;
+        c[r] = (ok && !pos[r]) ? v : 0.0f;
+      }
+      // stored tile: byte r of w_d = row r at this lane's column, each with its row's scale
+      unsigned w_d = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(c[r] * srow[r], 448.f), 0.f, 0, false) & 0xff;
+        w_d |= (unsigned)b << (8 * r);
+        const float dq = pos[r] ? cpos4[r] : q8_byte((unsigned)b, 0) * irow[r];
+        rdot[r] += dq * acc[mi][ni][r];
+      }
+      // mirror: 4 rows of column j, scaled by column j's row scale
+      const unsigned w_m = q8_pack4(c, scol[ni]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float dq = pos[r] ? cpos4[r] : q8_byte(w_m, r) * icol[ni];
+        cdot[ni] += dq * acc[mi][ni][r];
+      }
+      // quad byte swap: lane 4k + qd gathers row qd of columns 4k .. 4k+3 of this 16-column group
+      const unsigned s0 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0x00, 0xf, 0xf, false);  // quad_perm [k,k,k,k]
+      const unsigned s1 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0x55, 0xf, 0xf, false);
+      const unsigned s2 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0xaa, 0xf, 0xf, false);
+      const unsigned s3 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0xff, 0xf, 0xf, false);
+      const unsigned o = ((s0 >> (8 * qd)) & 0xffu) | (((s1 >> (8 * qd)) & 0xffu) << 8) |
+                         (((s2 >> (8 * qd)) & 0xffu) << 16) | (((s3 >> (8 * qd)) & 0xffu) << 24);
+      const int cl = cb[ni] - col_base + (lane & 12);  // first of the 4 columns (region-local)
+      *(__attribute__((address_space(3))) unsigned*)(ld_d + (row_t0 - row_base + qd) * S8 + cl) = o;
+      *(__attribute__((address_space(3))) unsigned*)(ld_m + (cb[ni] - col_base + (lane & 15)) * S8 +
+                                                    (row_t0 - row_base)) = w_m;
+    }
+    if (p.dotp) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float d = row16_sum(rdot[r]);
+        if ((lane & 15) == 0) p.dotp[(long long)(gi0 + r) * nslot + nt * 4 + wq] = d;
+      }
+    }
+  }
+  if (p.dotp && kind == kTileSymOff) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const float d = xrow_sum(cdot[ni]);
+      const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
+      if (lane < 16) p.dotp[(long long)row * nslot + (p.row_tile0 + mt) * 4 + (row_base >> 6)] = d;
+    }
+  }
+  __syncthreads();
+  // 64 rows x 64 B of each tile: lane l moves 16-B chunk (l & 3) of rows l >> 2 + 16 q
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = (lane >> 2) + 16 * q, c16 = lane & 3;
+    const u32x4 v = *(__attribute__((address_space(3))) const u32x4*)(ld_d + row * S8 + c16 * 16);
+    *reinterpret_cast<u32x4*>(slot + (row_base + row) * kTile + col_base + c16 * 16) = v;
+    if (mirror) {
+      const u32x4 m = *(__attribute__((address_space(3))) const u32x4*)(ld_m + row * S8 + c16 * 16);
+      *reinterpret_cast<u32x4*>(mirror + (col_base + row) * kTile + row_base + c16 * 16) = m;
+    }
+  }
+}
+
 // Block-scaled fp8 MFMA with the scale bytes selected by op_sel: byte IA of sa, byte IB of sb
 // (the builtin's op_sel operands must be literals).
 template <int IA, int IB>
 __device__ __forceinline__ f32x4 mma_mx_c(const i32x8& a, const i32x8& b, f32x4 c, int sa, int sb) {
   // cbsz = blgp = 0: both operands fp8 e4m3
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, IA, sa, IB, sb);
+}
+
+// ------------------------------------------------------------------------------------
+// Stream-K fixup of a partial K-range of tile `stile` (shared by the similarity GEMM and the
+// symmetric dZ GEMM; acc in the GEMM's fragment order, wave w = 4 wa + wb of 8). Returns true
+// when this block now holds the complete tile in acc and runs the epilogue.
+// ------------------------------------------------------------------------------------
+template <bool kF8>
+__device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[8][4], const SimParams& p, int stile, int bid, int G, int tid,
+                                         char* smem) {
+  const int lane = tid & 63, w = tid >> 6;
+  const int nk = p.nk;
+  // ---- stream-K fixup: partial K-range of tile `stile` -------------------------------
+  // Publish the fp32 partial (fragment order, 256 KiB) with write-through (sc1) 16-B
+  // stores, drain every wave, then one lane counts the arrival. The last arriver sums the
+  // segments in block order with sc1 loads (MI355X_MICROARCH.md § visibility, Valid forms
+  // row 1: sc1 payload both sides + ticket, so neither an agent release — whose L2
+  // write-back of every dirty line of the XCD cost ~30 us per episode here — nor an
+  // acquire). Its own segment stays in registers: fp32 addition is commutative, so
+  // ((s_b0 + s_b1) + s_b2) ... comes out bitwise identical whoever arrives last.
+  const int b0 = (int)((long long)stile * nk / p.ipb);
+  const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
+  auto slot_off = [&](int bb) {  // byte offset of block bb's slab for this tile
+    const long long s = (long long)bb * p.ipb;
+    const bool first_partial = (s / nk == stile) && (s % nk != 0);
+    return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
+  };
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
+  const unsigned lane_off = (unsigned)((w * 32 * 64 + lane) * 16);
+  {
+    const unsigned mine = slot_off(bid) + lane_off;
+#pragma unroll
+    for (int f = 0; f < 32; ++f) {
+      const f32x4 a = acc[f >> 2][f & 3];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), srs, (int)(mine + f * 64 * 16), 0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (p.sk_out) return false;  // split-K: the reduce launch finishes the tile
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == b1 - b0;
+    // every contributor has arrived: return the counter to zero for the next launch
+    if (last) __hip_atomic_store(p.sk_cnt + stile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  __syncthreads();
+  if (!last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  // The own segment stays in registers when it is the first or second term of the sum
+  // ((s_b0 + s_me) = (s_me + s_b0) bitwise); a later position re-reads it from its slab.
+  const bool reload_all = bid - b0 >= 2;
+  if constexpr (kF8) {
+    // (the pipelined form below made hipcc spill ~0.5 KiB per lane in the fp8 kernels)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      for (int bb = b0; bb <= b1; ++bb) {
+        if (bb == bid && !reload_all) continue;
+        const unsigned off = slot_off(bb) + lane_off;
+        u32x4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(off + (g * 8 + j) * 64 * 16), 0, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
+          f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
+          a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
+        }
+      }
+    }
+  } else {
+    // Slab reads are software-pipelined: the next contributor's 8 loads are in flight while the
+    // current ones are added (one serial round trip per (g, slab) made the fixup of a tile split
+    // 7 ways ~14 us at d = 8192). The next index is clamped, not branched on, so no load is
+    // conditional (hipcc would wait vmcnt(0) around it).
+    auto next_bb = [&](int bb) {
+      int nb = bb + 1;
+      if (nb == bid && !reload_all) ++nb;
+      return nb;
+    };
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      int bb = (b0 == bid && !reload_all) ? b0 + 1 : b0;  // <= b1: the last arriver is never alone
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(slot_off(bb) + lane_off + (g * 8 + j) * 64 * 16), 0, 16);
+      for (;;) {
+        const int nb = next_bb(bb);
+        const bool more = nb <= b1;
+        const unsigned noff = slot_off(more ? nb : bb) + lane_off;
+        u32x4 nv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          nv[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(noff + (g * 8 + j) * 64 * 16), 0, 16);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
+          f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
+          a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
+        }
+        if (!more) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = nv[j];
+        bb = nb;
+      }
+    }
+  }
+  return true;
+}
+
+// fp8 backward dZ (e4m3 C rows scaled by 2^e_m, e4m3 Z^T by 256): dequantise per row and add the
+// positive term C_mp z_p exactly from the fp16 rows (it is stored as 0 in the e4m3 C), after the
+// stream-K fixup (the finishing block only), before dz_store.
+__device__ __forceinline__ void dz8_finish(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt,
+                                           const int (&rb)[8], const int (&cb)[4], int lane) {
+  const float lmin = p.q8_lmin[0];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = mt * kTile + rb[mi] + (lane & 15);
+    const bool mv = m < p.R;
+    const float f = exp2i(-q8_row_exp(p.q8_mneg[m], lmin) - 8);
+    const float cp = mv ? p.cpos[m] : 0.f;
+    const int pm = mv ? (m < p.n_half ? m + p.n_half : m - p.n_half) : 0;
+    const _Float16* zp = p.q8_zq + (long long)pm * p.q8_ldz;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = nt * kTile + cb[ni] + 4 * (lane >> 4);
+      union { _Float16 h[4]; u32x2 u; } z4;
+      z4.u = (mv && n < p.q8_ldz) ? *reinterpret_cast<const u32x2*>(zp + n) : u32x2{0u, 0u};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[mi][ni][r] = acc[mi][ni][r] * f + cp * (float)z4.h[r];
+    }
+  }
+}
+
+// dZ epilogue (swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r])
+// of output tile (mt, nt); `lds` (>= 128 KiB, free) stages the fp16 tile for coalesced rows.
+__device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
+                                         const int (&rb)[8], const int (&cb)[4], lds_char* lds) {
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  const int lane = tid & 63;
+  // swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r]
+  float* out = p.out;
+  if (p.out_f16 && !p.accum) {
+    // fp16 tile through LDS (free after the main loop): fragments -> row-major [256][256] with
+    // the 16-byte chunk index XORed by (row & 15) (conflict-free both ways), then 512-byte
+    // coalesced rows out. A fragment's direct 8-byte stores put 16 rows in every instruction.
+    typedef __attribute__((address_space(3))) u32x2 lds_u2;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int rt = rb[mi] + (lane & 15);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int ct = cb[ni] + 4 * (lane >> 4);
+        union { _Float16 h[4]; u32x2 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
+        *(lds_u2*)(lds + rt * 512 + ((((ct >> 3) ^ (rt & 15))) << 4) + ((ct >> 2) & 1) * 8) = pk.u;
+      }
+    }
+    __syncthreads();
+    if (p.ndh) {
+      // Fused normalisation backward (replaces the norm_bwd launch and the dZ slab round trip):
+      //   dh = c1 * g - c2 * h,  c1 = s inv_m, c2 = s inv_m^2 dot_m,  s = grad_out / (2N tau),
+      // with dot_m = z_m . g_m = sum_j C_mj cos_mj from the coefficient pass. g is the fp16 tile
+      // staged above (the precision of the unfused fp16 dZ slab).
+      const float sgo = p.ngo[0] * p.nalpha;
+      typedef __attribute__((address_space(3))) float lds_fl;
+      lds_fl* cf = (lds_fl*)(lds + kTile * 512);  // [256][2] per-row c1, c2
+      if (tid < kTile) {
+        const int m = mt * kTile + tid;
+        const float iv = m < p.R ? p.ninv[m] : 0.f;
+        const float dt = m < p.R ? p.ndot[m] : 0.f;
+        cf[2 * tid] = sgo * iv;
+        cf[2 * tid + 1] = sgo * iv * iv * dt;
+      }
+      __syncthreads();
+#pragma unroll 2
+      for (int k = 0; k < 16; ++k) {
+        const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
+        const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
+        if (m >= p.R || d0 >= p.nd) continue;
+        union { _Float16 h[8]; u32x4 u; } g;
+        g.u = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
+        const float c1 = cf[2 * rt], c2 = cf[2 * rt + 1];
+        const long long off = (long long)m * p.nd + d0;
+        float hv[8], o[8];
+        if (p.nh_dt == 2) {
+          union { __bf16 h[8]; u32x4 u; } x;
+          x.u = *reinterpret_cast<const u32x4*>(static_cast<const __bf16*>(p.nh) + off);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
+        } else if (p.nh_dt == 1) {
+          union { _Float16 h[8]; u32x4 u; } x;
+          x.u = *reinterpret_cast<const u32x4*>(static_cast<const _Float16*>(p.nh) + off);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
+        } else {
+          const f32x4* hp = reinterpret_cast<const f32x4*>(static_cast<const float*>(p.nh) + off);
+          const f32x4 a = hp[0], b = hp[1];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { hv[e] = a[e]; hv[4 + e] = b[e]; }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = c1 * (float)g.h[e] - c2 * hv[e];
+        if (p.nh_dt == 2) {
+          union { __bf16 h[8]; u32x4 u; } y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y.h[e] = (__bf16)o[e];
+          *reinterpret_cast<u32x4*>(static_cast<__bf16*>(p.ndh) + off) = y.u;
+        } else if (p.nh_dt == 1) {
+          union { _Float16 h[8]; u32x4 u; } y;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) y.h[e] = (_Float16)o[e];
+          *reinterpret_cast<u32x4*>(static_cast<_Float16*>(p.ndh) + off) = y.u;
+        } else {
+          f32x4* op = reinterpret_cast<f32x4*>(static_cast<float*>(p.ndh) + off);
+          op[0] = f32x4{o[0], o[1], o[2], o[3]};
+          op[1] = f32x4{o[4], o[5], o[6], o[7]};
+        }
+      }
+      return;
+    }
+    _Float16* o16 = reinterpret_cast<_Float16*>(out) + ((long long)mt * kTile) * p.ldo + nt * kTile;
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
+      const u32x4 v = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
+      *reinterpret_cast<u32x4*>(o16 + (long long)rt * p.ldo + c * 8) = v;
+    }
+  } else {
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const long long row = (long long)mt * kTile + rb[mi] + (lane & 15);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int col = nt * kTile + cb[ni] + 4 * (lane >> 4);
+      if (p.out_f16) {
+        union { _Float16 h[4]; u32x2 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
+        *reinterpret_cast<u32x2*>(reinterpret_cast<_Float16*>(out) + row * p.ldo + col) = pk.u;
+      } else {
+        f32x4* o = reinterpret_cast<f32x4*>(out + row * p.ldo + col);
+        *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
+      }
+    }
+  }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -262,7 +711,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // fp8: 2 KiB more hold the dwords carrying the tile's 256 A-row and 256 B-row E8M0 scales (one
   // array: a second __shared__ object makes hipcc drain the LDS-DMA before every ds_read)
   constexpr int kScaleLds = MODE == kModeCoef ? kCoefLds : kGemmLds;
-  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + (std::is_same<T, fp8e4m3>::value ? 2048 : 0)];
+  // (+2 KiB: fp8 row scales, or the fused dZ epilogue's per-row coefficients)
+  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + ((std::is_same<T, fp8e4m3>::value || MODE == kModeDz) ? 2048 : 0)];
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
@@ -355,11 +805,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     __builtin_amdgcn_s_setprio(1);
     if constexpr (kF8) {
       // one block-scaled MFMA per (row block, column block) over the whole 128-element K-step
-      static_assert(MODE != kModeDz, "fp8 operands are forward-only");
+      // (dZ: operands swapped, as the 16-bit path, for the epilogue's row-per-lane orientation)
       auto mx = [&](auto mi_c, auto ni_c) {  // op_sel (scale byte) must be a literal
         constexpr int mi = decltype(mi_c)::value, ni = decltype(ni_c)::value;
         f32x4& c = acc[qa * 4 + mi][qb * 2 + ni];
-        c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, kUnitScale, kUnitScale);
+        if constexpr (MODE == kModeDz)
+          c = mma_mx_c<qb * 2 + ni, mi>(bf[0][ni], af[0][mi], c, kUnitScale, kUnitScale);
+        else
+          c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, kUnitScale, kUnitScale);
         // The block-scaled MFMA intrinsic is not convergent, so LLVM's IR sinking moved every
         // cluster of a K-step into the loop latch (one 32-MFMA cluster, operands of all phases
         // live at once -> spills and a vmcnt(0) in the loop). An empty asm use pins it here.
@@ -457,7 +910,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   // prologue: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1 (the stream clamps keep the
   // trailing prefetches in bounds, so every wait count below is uniform)
-  if constexpr (kF8) {
+  if constexpr (kF8 && MODE != kModeDz) {
     // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
     // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a 4-byte
     // LDS-DMA issued before the half-tiles: the vmcnt(10) below retires it with A0(0), B0(0)
@@ -497,7 +950,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
   if (grp == 0) barrier();  // re-align the groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
-  if constexpr (kF8) {
+  if constexpr (kF8 && MODE != kModeDz) {
     // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact, before any stream-K sum (acc row = rb +
     // 4 (lane >> 4) + r: four consecutive scale dwords; column = cb + (lane & 15))
     typedef __attribute__((address_space(3))) const unsigned lds_u32;
@@ -533,161 +986,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) cb[ni] = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
 
-  if (nsteps != nk) {
-    // ---- stream-K fixup: partial K-range of tile `stile` -------------------------------
-    // Publish the fp32 partial (fragment order, 256 KiB) with write-through (sc1) 16-B
-    // stores, drain every wave, then one lane counts the arrival. The last arriver sums the
-    // segments in block order with sc1 loads (MI355X_MICROARCH.md § visibility, Valid forms
-    // row 1: sc1 payload both sides + ticket, so neither an agent release — whose L2
-    // write-back of every dirty line of the XCD cost ~30 us per episode here — nor an
-    // acquire). Its own segment stays in registers: fp32 addition is commutative, so
-    // ((s_b0 + s_b1) + s_b2) ... comes out bitwise identical whoever arrives last.
-    const int b0 = (int)((long long)stile * nk / p.ipb);
-    const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
-    auto slot_off = [&](int bb) {  // byte offset of block bb's slab for this tile
-      const long long s = (long long)bb * p.ipb;
-      const bool first_partial = (s / nk == stile) && (s % nk != 0);
-      return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
-    };
-    const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
-    const unsigned lane_off = (unsigned)((w * 32 * 64 + lane) * 16);
-    {
-      const unsigned mine = slot_off(bid) + lane_off;
-#pragma unroll
-      for (int f = 0; f < 32; ++f) {
-        const f32x4 a = acc[f >> 2][f & 3];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), srs, (int)(mine + f * 64 * 16), 0, 16);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (p.sk_out) {  // split-K forward: the reduce launch finishes the tile
-      continue;
-    }
-    int* flag = reinterpret_cast<int*>(smem);
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == b1 - b0;
-      // every contributor has arrived: return the counter to zero for the next launch
-      if (last) __hip_atomic_store(p.sk_cnt + stile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = last;
-    }
-    __syncthreads();
-    const bool last = flag[0] != 0;
-    __syncthreads();
-    if (!last) {
-      continue;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-    // The own segment stays in registers when it is the first or second term of the sum
-    // ((s_b0 + s_me) = (s_me + s_b0) bitwise); a later position re-reads it from its slab.
-    const bool reload_all = bid - b0 >= 2;
-    if constexpr (kF8) {
-      // (the pipelined form below made hipcc spill ~0.5 KiB per lane in the fp8 kernels)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        for (int bb = b0; bb <= b1; ++bb) {
-          if (bb == bid && !reload_all) continue;
-          const unsigned off = slot_off(bb) + lane_off;
-          u32x4 v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(off + (g * 8 + j) * 64 * 16), 0, 16);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
-            f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
-            a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
-          }
-        }
-      }
-    } else {
-      // Slab reads are software-pipelined: the next contributor's 8 loads are in flight while the
-      // current ones are added (one serial round trip per (g, slab) made the fixup of a tile split
-      // 7 ways ~14 us at d = 8192). The next index is clamped, not branched on, so no load is
-      // conditional (hipcc would wait vmcnt(0) around it).
-      auto next_bb = [&](int bb) {
-        int nb = bb + 1;
-        if (nb == bid && !reload_all) ++nb;
-        return nb;
-      };
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        int bb = (b0 == bid && !reload_all) ? b0 + 1 : b0;  // <= b1: the last arriver is never alone
-        u32x4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          v[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(slot_off(bb) + lane_off + (g * 8 + j) * 64 * 16), 0, 16);
-        for (;;) {
-          const int nb = next_bb(bb);
-          const bool more = nb <= b1;
-          const unsigned noff = slot_off(more ? nb : bb) + lane_off;
-          u32x4 nv[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            nv[j] = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(noff + (g * 8 + j) * 64 * 16), 0, 16);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const f32x4 x = __builtin_bit_cast(f32x4, v[j]);
-            f32x4& a = acc[(g * 8 + j) >> 2][(g * 8 + j) & 3];
-            a = (reload_all && bb == b0) ? x : (bb < bid && !reload_all) ? x + a : a + x;
-          }
-          if (!more) break;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = nv[j];
-          bb = nb;
-        }
-      }
-    }
-  }
+  if (nsteps != nk && !sk_fixup<kF8>(acc, p, stile, bid, G, tid, smem)) continue;
 
   if constexpr (MODE == kModeDz) {
-    // swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r]
-    float* out = p.out;
-    if (p.out_f16 && !p.accum) {
-      // fp16 tile through LDS (free after the main loop): fragments -> row-major [256][256] with
-      // the 16-byte chunk index XORed by (row & 15) (conflict-free both ways), then 512-byte
-      // coalesced rows out. A fragment's direct 8-byte stores put 16 rows in every instruction.
-      typedef __attribute__((address_space(3))) u32x2 lds_u2;
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int rt = rb[mi] + (lane & 15);
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int ct = cb[ni] + 4 * (lane >> 4);
-          union { _Float16 h[4]; u32x2 u; } pk;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
-          *(lds_u2*)(lds + rt * 512 + ((((ct >> 3) ^ (rt & 15))) << 4) + ((ct >> 2) & 1) * 8) = pk.u;
-        }
-      }
-      __syncthreads();
-      _Float16* o16 = reinterpret_cast<_Float16*>(out) + ((long long)mt * kTile) * p.ldo + nt * kTile;
-#pragma unroll 4
-      for (int k = 0; k < 16; ++k) {
-        const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
-        const u32x4 v = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
-        *reinterpret_cast<u32x4*>(o16 + (long long)rt * p.ldo + c * 8) = v;
-      }
-    } else {
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const long long row = (long long)mt * kTile + rb[mi] + (lane & 15);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int col = nt * kTile + cb[ni] + 4 * (lane >> 4);
-        if (p.out_f16) {
-          union { _Float16 h[4]; u32x2 u; } pk;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
-          *reinterpret_cast<u32x2*>(reinterpret_cast<_Float16*>(out) + row * p.ldo + col) = pk.u;
-        } else {
-          f32x4* o = reinterpret_cast<f32x4*>(out + row * p.ldo + col);
-          *o = p.accum ? *o + acc[mi][ni] : acc[mi][ni];
-        }
-      }
-    }
-    }
+    if constexpr (kF8) dz8_finish(acc, p, mt, nt, rb, cb, lane);
+    dz_store(acc, p, mt, nt, tid, rb, cb, lds);
   } else if constexpr (MODE == kModeCoef) {
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
@@ -879,9 +1182,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 // (canonical fragment order: 16 fragments of 512 B) -> C into the coefficient buffer. 9 KiB of
 // LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound), and 16
 // waves per tile keep a small problem's few tiles (36 at B = 1024/view) spread over the chip.
-template <typename T, bool PERM = true>
+template <typename T, bool PERM = true, bool Q8 = false>
 __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[sizeof(T) == 2 ? kCoefWaveLds : 16];
+  __shared__ __attribute__((aligned(16))) char smem[Q8 ? 2 * 64 * 80 : (sizeof(T) == 2 ? kCoefWaveLds : 16)];
   const int lane = threadIdx.x;
   const int idx = xcd_remap(blockIdx.x, gridDim.x);
   const int tidx = idx >> 4, w = (idx >> 1) & 7, half = idx & 1;
@@ -911,7 +1214,10 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
         }
       }
     }
-  coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  if constexpr (Q8)
+    coef_epilogue_q8<T>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+  else
+    coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1414,7 +1720,37 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
     // swapped orientation (as the dZ epilogue): out[m = rb + (lane & 15)][n = cb + 4 (lane >> 4) + r]
     const long long row = (long long)mt * kTile + rb + (lane & 15);
     const int col = nt * kTile + cb + 4 * (lane >> 4);
-    if (p.out_f16) {
+    if (p.ndh) {
+      // fused normalisation backward (as dz_store): g rounded to fp16 like the unfused slab
+      if (row >= p.R || col >= p.nd) return;  // (nd % 8 == 0: the 4 columns are all in or all out)
+      const float sgo = p.ngo[0] * p.nalpha, iv = p.ninv[row];
+      const float c1 = sgo * iv, c2 = sgo * iv * iv * p.ndot[row];
+      const long long off = row * p.nd + col;
+      float hv[4], o[4];
+      if (p.nh_dt == 0) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(static_cast<const float*>(p.nh) + off);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[r] = a[r];
+      } else {
+        union { _Float16 f[4]; __bf16 b[4]; u32x2 u; } x;
+        x.u = *reinterpret_cast<const u32x2*>(static_cast<const char*>(p.nh) + off * 2);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hv[r] = p.nh_dt == 1 ? (float)x.f[r] : (float)x.b[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = c1 * (float)(_Float16)v[r] - c2 * hv[r];
+      if (p.nh_dt == 0) {
+        *reinterpret_cast<f32x4*>(static_cast<float*>(p.ndh) + off) = f32x4{o[0], o[1], o[2], o[3]};
+      } else {
+        union { _Float16 f[4]; __bf16 b[4]; u32x2 u; } y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (p.nh_dt == 1) y.f[r] = (_Float16)o[r];
+          else y.b[r] = (__bf16)o[r];
+        }
+        *reinterpret_cast<u32x2*>(static_cast<char*>(p.ndh) + off * 2) = y.u;
+      }
+    } else if (p.out_f16) {
       union { _Float16 h[4]; u32x2 u; } pk;
 #pragma unroll
       for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)v[r];

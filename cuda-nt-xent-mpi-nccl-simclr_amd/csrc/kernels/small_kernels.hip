@@ -6,8 +6,11 @@
 // (/root/reference/python/test.py:57-79). At these sizes the large-problem pipeline (256 x 256
 // persistent tiles, seven launches) is launch- and padding-bound; here:
 //
-//   small_fwd : grid (col block J, row block I) of 64 x 64 tiles, K = dim_k staged whole in LDS
-//               (global_load_lds, XOR-swizzled 16-B chunks), 16x16x32 MFMA (4 waves, 32 x 32
+//   small_fwd : grid (col block J, row block I) of 64 x 64 tiles. The row prologue is fused:
+//               each tile reads its two row blocks of h, L2-normalises and rounds them into LDS
+//               (XOR-swizzled 16-B chunks, K = dim_k whole); the diagonal tile also writes zq and
+//               1/|h| for the backward, and the tile holding a row's partner writes the positive
+//               logit. 16x16x32 MFMA (4 waves, 32 x 32
 //               each), masked per-row (max, sum) partials; the last-arriving tile of a row block
 //               merges that block's partials (finish_row: LSE, softplus loss term, positive
 //               weight a = 1 - P_ip) and the last row block sums the loss in block order
@@ -35,7 +38,11 @@ struct SmallParams {
   const void* zq;     // [Rpad][ldk] normalised rows, compute dtype (zero padded)
   const void* h;      // [R][d] input (backward)
   const float* inv;   // [R]
-  const float* ypos;  // [R] positive logit, log2 units
+  const void* hin;    // [R][d] input rows (forward: the fused row prologue reads them)
+  int hvec;           // hin rows can be read in 16-B vectors (d % 8 == 0, 16-B aligned base)
+  void* zq_out;       // [Rp64][ldk] zq written by the forward's diagonal tiles (backward operand)
+  float* inv_out;     // [R] 1/|h_i| written by the forward's diagonal tiles
+  float* ypos;        // [Rp64] positive logit (log2 units), written by the tile holding the pair
   float2* part;       // [nT][Rp64] per-(column block, row) (max, sum), log2 units
   float* lse2;        // [Rp64] full LSE (log2 units, positive included)
   float* arow;        // [Rp64] a_i = 1 - P_i,p(i)
@@ -74,10 +81,62 @@ __device__ __forceinline__ void stage_rows(const char* zq, long long ld_bytes, i
   }
 }
 
+// Fused row prologue: rows [row0, row0 + 64) of h, L2-normalised and rounded to T, into the
+// same swizzled LDS image as stage_rows (zero for rows >= R and columns >= d). 4 threads per
+// row, thread q of a row owning the 16-B chunks q, q + 4, ...; the row's sum of squares is
+// reduced over those 4 lanes. With zq_out set the rounded rows also go to zq (rows up to the
+// 64-row pad, zeros included) and 1/|h| to inv_out.
+template <typename Tin, typename T, int NKS>
+__device__ __forceinline__ void norm_stage(const Tin* h, int R, int d, bool vec, int row0, lds_char* dst, int tid,
+                                           T* zq_out, int ldk, float* inv_out) {
+  const int r = tid >> 2, q = tid & 3, gr = row0 + r;
+  const bool ok = gr < R;
+  const Tin* hr = h + (long long)gr * d;
+  float v[NKS][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NKS; ++k) {
+    const int e0 = 8 * (q + 4 * k);
+    if (ok && vec && e0 < d) {  // (d % 8 == 0: the whole chunk is in the row)
+      if constexpr (sizeof(Tin) == 4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(hr + e0), b = *reinterpret_cast<const f32x4*>(hr + e0 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[k][j] = a[j]; v[k][4 + j] = b[j]; }
+      } else {
+        union { u32x4 u; Tin x[8]; } pk;
+        pk.u = *reinterpret_cast<const u32x4*>(hr + e0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = to_f32<Tin>(pk.x[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = (ok && e0 + j < d) ? to_f32<Tin>(hr[e0 + j]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
+  }
+  ss += __shfl_xor(ss, 1, 64);
+  ss += __shfl_xor(ss, 2, 64);
+  const float iv = 1.0f / fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+  for (int k = 0; k < NKS; ++k) {
+    const int c = q + 4 * k;
+    union { u32x4 u; T x[8]; } pk;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pk.x[j] = from_f32<T>(v[k][j] * iv);
+    *(__attribute__((address_space(3))) u32x4*)(dst + sw_off<NKS>(r, c)) = pk.u;
+    if (zq_out) *reinterpret_cast<u32x4*>(zq_out + (long long)gr * ldk + 8 * c) = pk.u;
+  }
+  if (zq_out && ok && q == 0) inv_out[gr] = iv;
+}
+
 // ---------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------
-template <typename T, int NKS>
+// FUSE: the row prologue runs inside (norm_stage, above); otherwise launch_prep has written zq
+// and the positive logits, and the row blocks are staged from zq by LDS-DMA (large row counts:
+// a tile per 64 x 64 block re-normalising its rows costs more than the extra launch).
+template <typename Tin, typename T, int NKS, bool FUSE>
 __global__ __launch_bounds__(kSmallThreads) void small_fwd_kernel(const SmallParams p) {
   typedef typename Mfma<T>::frag frag;
   constexpr int RB = NKS * 64;
@@ -87,11 +146,21 @@ __global__ __launch_bounds__(kSmallThreads) void small_fwd_kernel(const SmallPar
   lds_char* lds = (lds_char*)smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int J = blockIdx.x, I = blockIdx.y;
-  const long long ldb = (long long)p.ldk * 2;
-  const char* zq = static_cast<const char*>(p.zq);
-  stage_rows<NKS>(zq, ldb, I * kSmallTile, lds, w, lane);
-  stage_rows<NKS>(zq, ldb, J * kSmallTile, lds + kSmallTile * RB, w, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const Tin* h = static_cast<const Tin*>(p.hin);
+  // row block I (A) and J (B); the diagonal tile stages one block, used as both operands, and
+  // publishes it (zq, inv) for the backward
+  lds_char* bimg = lds + (I == J ? 0 : kSmallTile * RB);
+  if constexpr (FUSE) {
+    norm_stage<Tin, T, NKS>(h, p.R, p.d, p.hvec != 0, I * kSmallTile, lds, tid,
+                            I == J ? static_cast<T*>(p.zq_out) : nullptr, p.ldk, p.inv_out);
+    if (I != J) norm_stage<Tin, T, NKS>(h, p.R, p.d, p.hvec != 0, J * kSmallTile, bimg, tid, nullptr, p.ldk, nullptr);
+  } else {
+    const long long ldb = (long long)p.ldk * 2;
+    const char* zq = static_cast<const char*>(p.zq);
+    stage_rows<NKS>(zq, ldb, I * kSmallTile, lds, w, lane);
+    if (I != J) stage_rows<NKS>(zq, ldb, J * kSmallTile, bimg, w, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
 
   const int wr = w >> 1, wc = w & 1, r16 = lane & 15, g = lane >> 4;
@@ -111,7 +180,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_fwd_kernel(const SmallPar
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
       const int row = 32 * wc + 16 * ni + r16;
-      b[ni] = *(__attribute__((address_space(3))) const frag*)(lds + kSmallTile * RB + sw_off<NKS>(row, 4 * ks + g));
+      b[ni] = *(__attribute__((address_space(3))) const frag*)(bimg + sw_off<NKS>(row, 4 * ks + g));
     }
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -134,6 +203,10 @@ __global__ __launch_bounds__(kSmallThreads) void small_fwd_kernel(const SmallPar
         const int gj = J * kSmallTile + 32 * wc + 16 * ni + r16;
         const bool drop = (gi >= p.R) | (gj >= p.R) | (gj == gi) | (gj == gpos);
         y[ni] = drop ? kNegInf : acc[mi][ni][r] * M;
+        // the positive pair lives in exactly one tile of the row: publish its logit (write-through,
+        // read by the row block's last arriver after the ticket below)
+        if (FUSE && gj == gpos && gi < p.R) __hip_atomic_store(p.ypos + gi, acc[mi][ni][r] * M, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
       }
       float m = row16_max(fmaxf(y[0], y[1]));
       const float ms = m == kNegInf ? 0.f : m;
@@ -197,7 +270,7 @@ __global__ __launch_bounds__(kSmallThreads) void small_fwd_kernel(const SmallPar
     for (int q2 = 1; q2 < 4; ++q2) lse_merge(v.x, v.y, red[q2][tid].x, red[q2][tid].y);
     if (gi < p.R) {
       const float m = v.x, s = v.y;
-      const float yp = p.ypos[gi];
+      const float yp = FUSE ? __hip_atomic_load(p.ypos + gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : p.ypos[gi];
       const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
       const float mx = fmaxf(neg2, yp);
       p.lse2[gi] = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
@@ -451,7 +524,7 @@ size_t small_scratch_bytes(const Geometry& g, int splits) {
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t part = (size_t)nt * nt * dev::kSmallTile * sizeof(float2);
   const size_t slabs = splits > 1 ? (size_t)nt * splits * dev::kSmallTile * g.dim_k * 4 : 0;
-  return up(ints * 4) + up(part) + up((size_t)nt * 4) + slabs;
+  return up(ints * 4) + up(part) + up((size_t)nt * 4) + up((size_t)nt * dev::kSmallTile * 4) + slabs;
 }
 
 namespace {
@@ -466,6 +539,8 @@ dev::SmallParams small_params(const Geometry& g, const void* zq, void* scratch, 
   b += up((size_t)nt * nt * dev::kSmallTile * sizeof(float2));
   p.loss_part = reinterpret_cast<float*>(b);
   b += up((size_t)nt * 4);
+  p.ypos = reinterpret_cast<float*>(b);
+  b += up((size_t)nt * dev::kSmallTile * 4);
   p.slabs = reinterpret_cast<float*>(b);
   p.zq = zq;
   p.R = g.rows;
@@ -496,21 +571,46 @@ void by_nks(int dk, F&& f) {
 
 int small_rows_pad(const Geometry& g) { return small_nt(g) * dev::kSmallTile; }
 
-void launch_small_fwd(DType comp, const void* zq, const float* ypos, float* lse2, float* arow, float* loss,
-                      void* scratch, const Geometry& g, hipStream_t stream) {
+bool small_fwd_fused(const Geometry& g) {
+  const int o = small_fuse_rows_override();
+  return g.rows <= (o >= 0 ? o : kSmallFuseMaxRows);
+}
+
+void launch_small_fwd(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos, float* lse2,
+                      float* arow, float* loss, void* scratch, const Geometry& g, hipStream_t stream) {
   NTXENT_CHECK(small_path_eligible(g, comp), "small path: problem not eligible");
   dev::SmallParams p = small_params(g, zq, scratch, 1);
-  p.ypos = ypos;
+  const bool fuse = small_fwd_fused(g);
+  NTXENT_CHECK(fuse || ypos != nullptr, "small forward (unfused): launch_prep's positive logits required");
+  if (!fuse) p.ypos = ypos;
+  p.hin = h;
+  p.hvec = (g.dim % 8 == 0) && (reinterpret_cast<uintptr_t>(h) % 16 == 0);
+  p.zq_out = zq;
+  p.inv_out = inv;
   p.lse2 = lse2;
   p.arow = arow;
   p.loss = loss;
   const dim3 grid(p.nT, p.nT);
   by_nks(g.dim_k, [&](auto nks) {
     constexpr int NKS = decltype(nks)::value;
-    if (comp == DType::F16)
-      hipLaunchKernelGGL((dev::small_fwd_kernel<_Float16, NKS>), grid, dim3(dev::kSmallThreads), 0, stream, p);
-    else
-      hipLaunchKernelGGL((dev::small_fwd_kernel<__bf16, NKS>), grid, dim3(dev::kSmallThreads), 0, stream, p);
+    auto go = [&](auto tin, auto tc) {
+      using Tin = decltype(tin);
+      using Tc = decltype(tc);
+      if (fuse)
+        hipLaunchKernelGGL((dev::small_fwd_kernel<Tin, Tc, NKS, true>), grid, dim3(dev::kSmallThreads), 0, stream, p);
+      else  // (zq is already in the compute dtype: the input dtype plays no part)
+        hipLaunchKernelGGL((dev::small_fwd_kernel<Tc, Tc, NKS, false>), grid, dim3(dev::kSmallThreads), 0, stream, p);
+    };
+    auto by_in = [&](auto tc) {
+      switch (in) {
+        case DType::F32: go(float{}, tc); break;
+        case DType::F16: go(_Float16{}, tc); break;
+        case DType::BF16: go(__bf16{}, tc); break;
+        default: NTXENT_CHECK(false, "small path: bad input dtype");
+      }
+    };
+    if (comp == DType::F16) by_in(_Float16{});
+    else by_in(__bf16{});
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
 #include <vector>
 
@@ -38,6 +39,12 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   bwd_ = backward_dtype(cfg.compute);
   cs_ = dtype_size(bwd_);
   small_ = cfg.small_path && world_ == 1 && small_path_eligible(g_, cfg.compute);
+  // dZ straight from the upper-triangular C and the (gathered) Zq rows: no ZqT, no mirrors
+  q8_ = !small_ && fp8_backward_eligible(g_, cfg.compute) &&
+        (cfg.fp8_backward < 0 ? fp8_backward_enabled() : cfg.fp8_backward != 0);
+  sym_ = !small_ && !q8_ && cfg.dz_sym && dz_sym_enabled() && dz_sym_eligible(g_, cfg.compute);
+  // normalisation backward fused into the dZ epilogue (the coefficient pass emits dot partials)
+  fuse_ = !small_ && bwd_ != DType::F32 && norm_fuse_enabled() && g_.dim % 8 == 0;
 
   const auto ft = build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -52,7 +59,10 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   const std::vector<Slot> slots = {
       {(void**)&zq_all_, W * Rp * g_.ld_k * cs_},
       {(void**)&zq8_all_, f8_ ? W * Rp * g_.ld_k8 : 0},
-      {(void**)&zqt_all_, W * g_.dim_n * g_.ld_t * cs_},
+      {(void**)&zqt_all_, (sym_ || q8_) ? 0 : W * g_.dim_n * g_.ld_t * cs_},
+      {(void**)&zq8t_, q8_ ? (size_t)g_.dim_n * (size_t)q8_ldt(g_) : 0},
+      {(void**)&q8_mneg_, q8_ ? Rp * 4 : 0},
+      {(void**)&q8_lmin_, q8_ ? (size_t)4 : (size_t)0},
       {(void**)&inv_, R * 4},
       {(void**)&ypos_, R * 4},
       {(void**)&part_, (size_t)g_.col_tiles * Rp * sizeof(float2)},
@@ -64,6 +74,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&loss_, 4},
       {(void**)&one_, 4},
       {(void**)&slabs_, Rp * g_.dim_n * 4},
+      {(void**)&dotp_, fuse_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
+      {(void**)&dot_, fuse_ ? Rp * 4 : 0},
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
       {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
       {&ws_.ptr, ws_.bytes},
@@ -117,16 +129,19 @@ void Engine::forward(const void* h, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.prep");
     fault_point("prep");
-    launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
-    if (small_) {  // one launch: tiles + LSE merge + loss (lse2 -> lse2_all_, a_i -> cpos_)
+    if (small_) {  // one launch (row prologue fused up to kSmallFuseMaxRows): tiles + LSE merge + loss
+      // (lse2 -> lse2_all_, a_i -> cpos_)
+      if (!small_fwd_fused(g_)) launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s);
       NTXENT_TRACE("ntxent.small_fwd");
       fault_point("fwd");
-      launch_small_fwd(cfg_.compute, zq_local, ypos_, lse2_all_, cpos_, loss_, small_scratch_, g_, s);
+      launch_small_fwd(cfg_.input, cfg_.compute, h, zq_local, inv_, ypos_, lse2_all_, cpos_, loss_, small_scratch_,
+                       g_, s);
       if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
       return;
     }
+    launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
     // world 1: the transpose is written by the LSE launch (beside the merge, see below)
-    if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
+    if (world_ > 1 && !sym_) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
@@ -134,7 +149,10 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_prep_, 0));
     comm_->all_gather(op_local, op_all, op_bytes, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zq_, comm_stream_));
-    comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
+    // the backward's B operand: ZqT blocks, or (dz_sym) the fp16 rows themselves — already
+    // gathered above unless the forward ran on the fp8 copy
+    if (!sym_) comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
+    else if (f8_) comm_->all_gather(zq_local, zq_all_, Rp * g_.ld_k * cs_, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
     zqt_pending_ = true;
   }
@@ -156,8 +174,16 @@ void Engine::forward(const void* h, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.lse");
     fault_point("lse");
-    if (world_ == 1) launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
-    else launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
+    if (q8_) {
+      Q8Stats q8;
+      q8.mneg2 = q8_mneg_;
+      q8.lmin = q8_lmin_;
+      q8.zq8t = zq8t_;
+      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
+    } else if (world_ == 1 && !sym_)
+      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
+    else
+      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
   }
   if (world_ > 1) {
     NTXENT_TRACE("ntxent.lse_gather");
@@ -172,6 +198,10 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   NTXENT_CHECK(h_ != nullptr, "backward() before forward()");
   const size_t Rp = g_.rows_pad;
   const char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
+  Q8Stats q8;  // fp8 backward (q8_)
+  q8.mneg2 = q8_mneg_;
+  q8.lmin = q8_lmin_;
+  q8.zq = zq_local;
   if (small_) {
     NTXENT_TRACE("ntxent.small_bwd");
     fault_point("dz");
@@ -183,9 +213,12 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");
     if (cfg_.keep_cos)
-      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s);
+      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr,
+                  /*upper_only=*/sym_ && !std::getenv("NTXENT_DZSYM_NOMIR"), dotp_, q8_ ? &q8 : nullptr);
     else
-      launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s);
+      launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
+                       BlockView{}, dotp_);
+    if (fuse_) launch_dot_reduce(dotp_, dot_, g_, s);
   }
   if (zqt_pending_) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));
@@ -194,7 +227,21 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.dz_gemm");
     fault_point("dz");
-    launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32);
+    NormFuse nf;
+    nf.h = h_;
+    nf.in = cfg_.input;
+    nf.inv = inv_;
+    nf.dot = dot_;
+    nf.grad_out = grad_out ? grad_out : one_;
+    nf.dh = dh;
+    const bool fused =
+        sym_ ? launch_dz_sym(cfg_.compute, cbuf_, zq_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
+                             fuse_ ? &nf : nullptr)
+        : q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
+                          fuse_ ? &nf : nullptr, &q8, cpos_)
+             : launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32,
+                         fuse_ ? &nf : nullptr);
+    if (fused) return;  // dh written by the dZ epilogue
   }
   {
     NTXENT_TRACE("ntxent.norm_bwd");

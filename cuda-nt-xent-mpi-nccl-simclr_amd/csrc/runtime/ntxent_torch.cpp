@@ -66,6 +66,7 @@ struct Plan {
   int n_dz = 0;
   int num_cus = 256;
   bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
+  bool dz_sym = false;  // dZ from the upper-triangular C and Zq itself (launch_dz_sym)
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
@@ -114,6 +115,7 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
   p->small = small_path_eligible(p->g, comp);
+  p->dz_sym = dz_sym_eligible(p->g, comp);
   cache.emplace(key, p);
   return p;
 }
@@ -287,29 +289,33 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
 }
 
 // Kept cosines (compact, one slot per forward tile) -> coefficient buffer (all tiles).
-at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P) {
+// upper_only: only the stored tiles (the layout dz_sym reads), no mirrored lower tiles.
+at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
+                bool upper_only = false, float* dotp = nullptr) {
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
-              reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf));
+              reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf), nullptr,
+              upper_only, dotp);
   return cbuf;
 }
 
 at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& lse2_all,
-                     const at::Tensor& cpos, const Plan& P) {
+                     const at::Tensor& cpos, const Plan& P, float* dotp = nullptr) {
   check_input(zq_local, "zq_local");
   const at::DeviceGuard guard(zq_local.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_coef_gemm(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(),
                    cpos.data_ptr<float>(), reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
-                   ws, P.g, cur_stream(zq_local));
+                   ws, P.g, cur_stream(zq_local), BlockView{}, dotp);
   return cbuf;
 }
 
-at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
+at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P, const NormFuse* nf = nullptr,
+              bool* fused = nullptr) {
   check_input(sc, "sc");
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
@@ -318,8 +324,10 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) {
   const bool f16 = P.bwd() != DType::F32;
   auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(sc, f16 ? at::kHalf : at::kFloat));
   auto ws = gemm_ws(sc, P.n_dz, P);
-  launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
-            P.n_dz, slabs.data_ptr(), ws, P.g, cur_stream(sc), f16);
+  const bool f = launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(),
+                           reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws, P.g,
+                           cur_stream(sc), f16, nf);
+  if (fused) *fused = f;
   return slabs;
 }
 
@@ -336,6 +344,27 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
     launch_norm_bwd(to_dtype(h.scalar_type()), slabs.data_ptr<float>(), 1, h.data_ptr(), inv.data_ptr<float>(),
                     go.data_ptr<float>(), dh.data_ptr(), P.g, cur_stream(h));
   return dh;
+}
+
+// dZ = C Zq from upper-triangular coefficient tiles (coef(..., upper_only=true) or coef_gemm)
+// and the normalised rows (no ZqT); fp16 slab.
+at::Tensor dz_sym(const at::Tensor& cbuf, const at::Tensor& zq_all, const Plan& P, const NormFuse* nf = nullptr,
+                  bool* fused = nullptr) {
+  check_input(cbuf, "cbuf");
+  check_input(zq_all, "zq_all");
+  NTXENT_CHECK(P.dz_sym, "dz_sym: plan not eligible (see dz_sym_eligible)");
+  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.g.ld_k && zq_all.scalar_type() == to_scalar(P.bwd()),
+               "zq_all must be [world*rows_pad, ld_k] in the backward dtype");
+  NTXENT_CHECK(cbuf.numel() == (long)P.g.row_tiles * P.g.col_tiles * kTileElems && cbuf.scalar_type() == to_scalar(P.bwd()),
+               "cbuf must be [row_tiles * col_tiles] tiles in the backward dtype");
+  const at::DeviceGuard guard(cbuf.device());
+  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(cbuf, at::kHalf));
+  auto ws = gemm_ws(cbuf, P.n_dz, P);
+  const bool f = launch_dz_sym(P.comp, cbuf.data_ptr(), zq_all.data_ptr(),
+                               reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws,
+                               P.g, cur_stream(cbuf), /*out_f16=*/true, nf);
+  if (fused) *fused = f;
+  return slabs;
 }
 
 // ---- ring-negatives stage ops (O(local) memory; parallel/ring.py) --------------------------
@@ -579,29 +608,60 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   // callers as an explicit "fp16".
   const DType comp = choose_compute(h.scalar_type(), false, compute);
   auto P = get_plan((int)h.size(0), (int)h.size(1), 1, 0, T, dtype_name(comp), h.device().index());
-  auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
   if (P->small && small_path_enabled()) {
-    // {loss, zq, -, inv, lse2, -, a}: the backward recomputes S from zq (small_bwd)
+    // {loss, zq, -, inv, lse2, -, a}: the backward recomputes S from zq (small_bwd). One launch:
+    // the forward kernel normalises the rows itself (small_fwd_fused) and writes zq / inv.
     const int rp = small_rows_pad(P->g);
     auto lse2 = at::empty({rp}, opts(h, at::kFloat));
     auto arow = at::empty({rp}, opts(h, at::kFloat));
     auto loss = at::empty({}, opts(h, at::kFloat));
-    launch_small_fwd(P->comp, pr[0].data_ptr(), pr[2].data_ptr<float>(), lse2.data_ptr<float>(),
-                     arow.data_ptr<float>(), loss.data_ptr<float>(), small_scratch(h, *P).data_ptr(), P->g,
-                     cur_stream(h));
-    return {loss, pr[0], at::Tensor(), pr[1], lse2, at::Tensor(), arow};
+    at::Tensor zq, inv;
+    float* ypos = nullptr;
+    if (small_fwd_fused(P->g)) {
+      zq = at::empty({rp, P->g.ld_k}, opts(h, to_scalar(P->comp)));
+      inv = at::empty({P->g.rows}, opts(h, at::kFloat));
+    } else {
+      auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
+      zq = pr[0];
+      inv = pr[1];
+      ypos = pr[2].data_ptr<float>();
+    }
+    launch_small_fwd(to_dtype(h.scalar_type()), P->comp, h.data_ptr(), zq.data_ptr(), inv.data_ptr<float>(), ypos,
+                     lse2.data_ptr<float>(), arow.data_ptr<float>(), loss.data_ptr<float>(),
+                     small_scratch(h, *P).data_ptr(), P->g, cur_stream(h));
+    return {loss, zq, at::Tensor(), inv, lse2, at::Tensor(), arow};
   }
-  // ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes it from
-  // extra blocks beside the merge (one stream: a side-stream transpose cost an event record and
-  // a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
-  auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
+  auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
+  // dz_sym plans read Zq itself in the backward (zqt returned EMPTY: the backward's marker).
+  // Otherwise ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes
+  // it from extra blocks beside the merge (one stream: a side-stream transpose cost an event
+  // record and a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
+  const bool sym = P->dz_sym && dz_sym_enabled();
+  auto zqt = sym ? at::empty({0}, pr[0].options()) : at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
   auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  if (f8 && fp8_backward_enabled() && fp8_backward_eligible(P->g, comp)) {
+    // fp8 backward: zqt = e4m3(256 Zq^T) (uint8: the backward's marker); cpos carries the LSE
+    // pass's Q8Stats after its Rpad entries: [cpos | mneg2 (Rpad) | lmin]
+    const long Rp = P->g.rows_pad;
+    auto cpos = at::empty({2 * Rp + 64}, opts(h, at::kFloat));
+    auto zq8t = at::empty({P->g.dim_n, q8_ldt(P->g)}, opts(h, at::kByte));
+    Q8Stats q8;
+    q8.mneg2 = cpos.data_ptr<float>() + Rp;
+    q8.lmin = cpos.data_ptr<float>() + 2 * Rp;
+    q8.zq8t = zq8t.data_ptr();
+    auto block_loss = device_scratch(h, (size_t)lse_scratch_floats(P->g) * 4, 1);
+    auto loss = at::empty({}, opts(h, at::kFloat));
+    launch_lse(reinterpret_cast<const float2*>(fs[0].data_ptr<float>()), pr[2].data_ptr<float>(), lse2.data_ptr<float>(),
+               cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()), loss.data_ptr<float>(), P->g,
+               cur_stream(h), DType::F16, pr[0].data_ptr(), nullptr, &q8);
+    return {loss, pr[0], zq8t, pr[1], lse2, fs[1], cpos};
+  }
   auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-  auto loss = lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
+  auto loss = sym ? lse(fs[0], pr[2], lse2, cpos, *P) : lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
@@ -622,14 +682,76 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
                      small_scratch(h, *P).data_ptr(), P->g, cur_stream(h), small_splits(*P));
     return dh;
   }
+  if (zqt.scalar_type() == at::kByte) {  // fp8 backward (see fused_forward)
+    const long Rp = P->g.rows_pad;
+    Q8Stats q8;
+    q8.mneg2 = const_cast<float*>(cpos.data_ptr<float>()) + Rp;
+    q8.lmin = const_cast<float*>(cpos.data_ptr<float>()) + 2 * Rp;
+    q8.zq = zq.data_ptr();
+    NTXENT_CHECK(sc_in.has_value() && sc_in->defined() && cpos.numel() == 2 * Rp + 64,
+                 "fused_backward (fp8): kept cosines and the forward's Q8Stats required");
+    const bool fuse = norm_fuse_enabled();
+    at::Tensor dotp, dot, dh, go;
+    if (fuse) {
+      dotp = at::empty({Rp * dot_slots(P->g)}, opts(h, at::kFloat));
+      dot = at::empty({Rp}, opts(h, at::kFloat));
+    }
+    auto cb = at::empty({(long)P->g.row_tiles * P->g.col_tiles * kTileElems}, opts(h, at::kByte));
+    launch_coef(DType::F16, sc_in->data_ptr(), cb.data_ptr(), lse2.data_ptr<float>(), cpos.data_ptr<float>(),
+                reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd, P->g, cur_stream(h), nullptr,
+                false, fuse ? dotp.data_ptr<float>() : nullptr, &q8);
+    NormFuse nf;
+    if (fuse) {
+      launch_dot_reduce(dotp.data_ptr<float>(), dot.data_ptr<float>(), P->g, cur_stream(h));
+      go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
+      dh = at::empty_like(h);
+      nf.h = h.data_ptr();
+      nf.in = to_dtype(h.scalar_type());
+      nf.inv = inv.data_ptr<float>();
+      nf.dot = dot.data_ptr<float>();
+      nf.grad_out = go.data_ptr<float>();
+      nf.dh = dh.data_ptr();
+    }
+    auto slabs = at::empty({1, P->g.rows_pad, P->g.dim_n}, opts(h, at::kHalf));
+    auto ws = gemm_ws(h, P->n_dz, *P);
+    const bool fused = launch_dz(DType::FP8, cb.data_ptr(), zqt.data_ptr(),
+                                 reinterpret_cast<const int4*>(P->dz_tiles.data_ptr<int>()), P->n_dz, slabs.data_ptr(),
+                                 ws, P->g, cur_stream(h), /*out_f16=*/true, fuse ? &nf : nullptr, &q8,
+                                 cpos.data_ptr<float>());
+    return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
+  }
+  const bool sym = zqt.numel() == 0;  // dz_sym forward (see fused_forward)
+  // dz_sym plans finish the normalisation backward in the dZ epilogue (norm_fuse_enabled): the
+  // coefficient pass also emits the partials of dot_i = z_i . g_i
+  const bool fuse = P->bwd() != DType::F32 && norm_fuse_enabled() && P->g.dim % 8 == 0;
+  at::Tensor dotp, dot;
+  if (fuse) {
+    dotp = at::empty({(long)P->g.rows_pad * dot_slots(P->g)}, opts(h, at::kFloat));
+    dot = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  }
+  float* dp = fuse ? dotp.data_ptr<float>() : nullptr;
   at::Tensor cb;
   if (sc_in.has_value() && sc_in->defined()) {
-    cb = coef(*sc_in, lse2, cpos, *P);
+    cb = coef(*sc_in, lse2, cpos, *P, /*upper_only=*/sym, dp);
   } else {
-    cb = coef_gemm(zq, zq, lse2, cpos, *P);
+    cb = coef_gemm(zq, zq, lse2, cpos, *P, dp);
   }
-  auto slabs = dz(cb, zqt, *P);
-  return norm_bwd(slabs, h, inv, grad_out, *P);
+  at::Tensor dh, go;
+  NormFuse nf;
+  if (fuse) {
+    launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
+    go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
+    dh = at::empty_like(h);
+    nf.h = h.data_ptr();
+    nf.in = to_dtype(h.scalar_type());
+    nf.inv = inv.data_ptr<float>();
+    nf.dot = dot.data_ptr<float>();
+    nf.grad_out = go.data_ptr<float>();
+    nf.dh = dh.data_ptr();
+  }
+  bool fused = false;
+  auto slabs = sym ? dz_sym(cb, zq, *P, fuse ? &nf : nullptr, &fused) : dz(cb, zqt, *P, fuse ? &nf : nullptr, &fused);
+  return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
 }
 
 // ---- reference-compatible API (src/binding_new.cpp:5-20) -------------------------------
@@ -704,7 +826,8 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
   auto pr = prep(z, *P, c10::nullopt, c10::nullopt);
-  auto zqt = transpose(pr[0], *P, c10::nullopt);
+  const bool sym = P->dz_sym && dz_sym_enabled();
+  auto zqt = sym ? at::Tensor() : transpose(pr[0], *P, c10::nullopt);
   const long R = z.size(0), n = R / 2, Rp = P->g.rows_pad;
   at::Tensor lse2, cpos;
   const bool have_lse = stats.defined() && stats.dim() == 1 && stats.size(0) == R && stats.is_floating_point() &&
@@ -726,7 +849,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
     lse(fs[0], pr[2], lse2, cpos, *P);
   }
   auto sc = coef_gemm(pr[0], pr[0], lse2, cpos, *P);
-  auto slabs = dz(sc, zqt, *P);
+  auto slabs = sym ? dz_sym(sc, pr[0], *P) : dz(sc, zqt, *P);
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
   auto dh = norm_bwd(slabs, z, pr[1], go, *P);
   at::Tensor grad_logits;
@@ -803,6 +926,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("small", &Plan::small)
+      .def_readonly("dz_sym", &Plan::dz_sym)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
   m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
@@ -818,9 +942,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fwd_stats", &fwd_stats, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"));
   m.def("lse", &lse, py::arg("part"), py::arg("ypos"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
         py::arg("zq") = py::none(), py::arg("zqt") = py::none());
-  m.def("coef", &coef);
-  m.def("coef_gemm", &coef_gemm);
-  m.def("dz", &dz);
+  m.def("coef", [](const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
+                   bool upper_only) { return coef(sbuf, lse2_all, cpos, P, upper_only); },
+        py::arg("sbuf"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("upper_only") = false);
+  m.def("coef_gemm", [](const at::Tensor& zl, const at::Tensor& za, const at::Tensor& lse2_all, const at::Tensor& cpos,
+                        const Plan& P) { return coef_gemm(zl, za, lse2_all, cpos, P); });
+  m.def("dz", [](const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) { return dz(sc, zqt_all, P); });
+  m.def("dz_sym", [](const at::Tensor& cbuf, const at::Tensor& zq_all, const Plan& P) { return dz_sym(cbuf, zq_all, P); },
+        py::arg("cbuf"), py::arg("zq_all"), py::arg("plan"));
+  m.def("set_dz_sym", &ntxent::set_dz_sym, py::arg("on"));
+  m.def("set_norm_fuse", &ntxent::set_norm_fuse, py::arg("on"));
+  m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
+  m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
+  m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
+  m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);
   m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
   m.def("set_splitk_reduce", &ntxent::set_splitk_reduce, py::arg("on"));
   m.def("set_diag_subtiles", &ntxent::set_diag_subtiles, py::arg("on"));
@@ -852,6 +987,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_small_path", &ntxent::set_small_path, py::arg("on"));
   m.def("small_path_enabled", &ntxent::small_path_enabled);
   m.def("set_small_splits", &ntxent::set_small_splits, py::arg("n"));
+  m.def("set_small_fuse_rows", &ntxent::set_small_fuse_rows, py::arg("rows"));
+  m.def("small_fwd_fused", [](const Plan& P) { return ntxent::small_fwd_fused(P.g); });
   // reference API names and kwargs
   m.def("forward", &forward_op, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);
   m.def("forward_with_stats", &forward_with_stats, py::arg("z"), py::arg("T"), py::arg("use_mixed_precision") = false);

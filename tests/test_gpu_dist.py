@@ -67,10 +67,15 @@ def _large_path():
 
     mod = _ext.load(build_if_missing=False)
     mod.set_small_path(False)
+    # (and the unfused normalisation backward: the emulated ranks run the data-parallel stage
+    # ops, whose dZ slab goes through launch_norm_bwd)
+    old_fuse = mod.norm_fuse_enabled()
+    mod.set_norm_fuse(False)
     try:
         yield
     finally:
         mod.set_small_path(True)
+        mod.set_norm_fuse(old_fuse)
 
 
 def test_emulated_world1_equals_single_gpu():

@@ -1,0 +1,57 @@
+"""fp8 backward (FP8 plans): the coefficient matrix and Z^T enter the dZ GEMM as e4m3 (per-row
+scale from the LSE pass's bound, Z^T scaled by 256) on the block-scaled MFMA, the positive term
+added exactly in the dZ epilogue. Gradient error against the host fp64 oracle, next to the
+fp8-forward / fp16-backward path of the same inputs (the error table in BASELINE.md comes from
+these prints)."""
+import pytest
+import torch
+
+from test_gpu_kernels import _inputs, _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _grad(h, T, fp8_bwd, fuse=True):
+    import ntxent_amd
+
+    C = ntxent_amd.ops._ext.load()
+    old, old_f = C.fp8_backward_enabled(), C.norm_fuse_enabled()
+    C.set_fp8_backward(fp8_bwd)
+    C.set_norm_fuse(fuse)
+    try:
+        x = h.clone().requires_grad_(True)
+        loss = ntxent_amd.ntxent_loss(x, T, compute="fp8", keep_logits=True)
+        (g,) = torch.autograd.grad(loss, x)
+        torch.cuda.synchronize()
+        return loss.item(), g
+    finally:
+        C.set_fp8_backward(old)
+        C.set_norm_fuse(old_f)
+
+
+@pytest.mark.parametrize("rows,dim,T", [
+    (4096, 512, 0.07),
+    (2048, 1024, 0.07),
+    (3000, 256, 0.1),    # padded rows
+    (4096, 256, 0.5),
+])
+def test_fp8_backward_error_vs_oracle(ext, rows, dim, T):
+    _, h = _inputs(rows, dim, torch.bfloat16, seed=rows + dim)
+    l8, g8 = _grad(h, T, True)
+    l16, g16 = _grad(h, T, False)
+    assert l8 == l16  # same forward
+    lref, gref = _oracle(h, T)
+    scale = gref.abs().max().item()
+    e8 = (g8.double().cpu() - gref).abs().max().item() / scale
+    e16 = (g16.double().cpu() - gref).abs().max().item() / scale
+    print(f"FP8BWD rows={rows} dim={dim} T={T}: max|g - g64|/max|g64| fp8-bwd {e8:.3e}  fp16-bwd {e16:.3e}")
+    assert torch.isfinite(g8).all()
+    assert e8 <= 5e-2, e8
+
+
+def test_fp8_backward_unfused_matches_fused(ext):
+    _, h = _inputs(4096, 512, torch.bfloat16, seed=3)
+    _, gf = _grad(h, 0.07, True, fuse=True)
+    _, gu = _grad(h, 0.07, True, fuse=False)
+    scale = gu.float().abs().max().item()
+    assert (gf.float() - gu.float()).abs().max().item() <= 1e-2 * scale

@@ -49,18 +49,23 @@ def _oracle(h, T, go=1.0):
 def small_on(ext):
     ext.set_small_path(True)
     ext.set_small_splits(0)
+    ext.set_small_fuse_rows(-1)
     yield ext
     ext.set_small_path(True)
     ext.set_small_splits(0)
+    ext.set_small_fuse_rows(-1)
 
 
+@pytest.mark.parametrize("fuse", [True, False])
 @pytest.mark.parametrize("compute", ["fp16", "bf16"])
 @pytest.mark.parametrize("in_dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("rows,dim", [(64, 128), (34, 100), (128, 256), (600, 200), (1024, 64), (2048, 256),
                                       (2048, 128), (66, 192)])
-def test_small_path_matches_oracle(small_on, rows, dim, in_dtype, compute):
+def test_small_path_matches_oracle(small_on, rows, dim, in_dtype, compute, fuse):
+    """fuse: the forward normalises the rows itself (one launch) or runs after launch_prep."""
+    small_on.set_small_fuse_rows(1 << 20 if fuse else 0)
     plan = small_on.get_plan(rows, dim, 1, 0, 0.07, compute, 0)
-    assert plan.small
+    assert plan.small and small_on.small_fwd_fused(plan) == fuse
     h = _inputs(rows, dim, in_dtype, seed=rows * 3 + dim)
     l, g = _run(h, 0.07, compute, go=0.7)
     lr, gr = _oracle(h, 0.07, go=0.7)
@@ -111,3 +116,20 @@ def test_small_path_stability_grid(small_on, scale, T):
     assert abs(l - lr) <= 2e-2 * max(1.0, abs(lr)), (l, lr)
     err = (grad.double().cpu() - gr).abs().max().item() / max(gr.abs().max().item(), 1e-30)
     assert err <= 6e-2, err
+
+
+@pytest.mark.parametrize("in_dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("rows,dim", [(256, 256), (130, 72), (1000, 128)])
+def test_small_fused_prologue_vs_prep(small_on, rows, dim, in_dtype):
+    """The one-launch forward (rows normalised in the kernel, positive logit taken from the MFMA
+    tile holding the pair) against the forward after launch_prep: same rounded rows, so the loss
+    agrees to accumulation order and the gradients (same backward) to output rounding (fp16 dh at
+    this scale is subnormal: one ulp is 2^-24)."""
+    h = _inputs(rows, dim, in_dtype, seed=rows + dim)
+    small_on.set_small_fuse_rows(1 << 20)
+    lf, gf = _run(h, 0.07, "fp16")
+    small_on.set_small_fuse_rows(0)
+    lp, gp = _run(h, 0.07, "fp16")
+    assert abs(lf - lp) <= 1e-5 * abs(lp), (lf, lp)
+    diff = (gf.float() - gp.float()).abs().max().item()
+    assert diff <= max(2e-3 * gp.float().abs().max().item(), 2 * 2.0 ** -24), diff

@@ -1,15 +1,11 @@
 #!/bin/bash
-# Small-problem path on the GPU box: its tests, the kernel tests, and the reference sweep on
-# the native bench with and without the small path. usage: tools/gpu_small.sh TAG
+# Reference forward-latency sweep (B {32..1024} x D {64,128,256}, host fp64 check) with the fused
+# one-launch small forward (default) and with the prep launch (--small-fuse-rows 0), plus graphs.
 set -o pipefail
-export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-small}; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_small.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest_small.log 2>&1 || { echo "small tests failed"; tail -40 $OUT/pytest_small.log; exit 1; }
-tail -1 $OUT/pytest_small.log
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest_kernels.log 2>&1 || { echo "kernel tests failed"; tail -40 $OUT/pytest_kernels.log; exit 1; }
-tail -1 $OUT/pytest_kernels.log
-timeout -k 10 200 build/bin/ntxent_bench --iters 50 --check > $OUT/refsweep_small.log 2>&1 || { echo "sweep failed"; tail -20 $OUT/refsweep_small.log; exit 1; }
-timeout -k 10 200 build/bin/ntxent_bench --iters 50 --graph > $OUT/refsweep_graph.log 2>&1 || { echo "sweep graph failed"; tail -20 $OUT/refsweep_graph.log; exit 1; }
-timeout -k 10 200 build/bin/ntxent_bench --iters 50 --no-small > $OUT/refsweep_large.log 2>&1 || { echo "sweep large failed"; tail -20 $OUT/refsweep_large.log; exit 1; }
-awk -F"|" "NR>2 && NF>4 {print \$1 \"|\" \$4 \"|\" \$5}" $OUT/refsweep_graph.log
-echo done
+for v in "" "--small-fuse-rows 0" "--graph"; do
+  t=$(echo "fused$v" | tr -d ' -')
+  timeout -k 10 240 build/bin/ntxent_bench --check $v --iters 200 --warmup 20 > $OUT/$t.log 2>&1 || { echo "sweep $v failed"; tail $OUT/$t.log; exit 1; }
+  echo "== $t"; grep -E "^ +[0-9]+ +[0-9]+ " $OUT/$t.log | awk '{print $1, $2, $4, "fwd", $6, "bwd", $11, "fb", $16, "graph", $21}'
+  grep -iE "check|max" $OUT/$t.log | tail -3
+done
