@@ -143,9 +143,10 @@ void* upload(std::vector<float>& host, DType in) {
 class Bench {
  public:
   Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed,
-        bool small_path = true, int small_splits = 0)
+        bool small_path = true, int small_splits = 0, Negatives neg = Negatives::kSymmetric)
       : in_(in) {
     EngineConfig c;
+    c.negatives = neg;
     c.rows = 2 * batch;
     c.dim = dim;
     c.temperature = T;
@@ -263,6 +264,8 @@ struct Options {
   float T = 0.07f;
   bool check = false, graph = false, recompute = false, small = true;
   int small_splits = 0;
+  Negatives negatives = Negatives::kSymmetric;
+  bool emulate = false;  // --gpus N as N emulated ranks on GPU 0 (ThreadComm), not N GPUs over RCCL
 };
 
 // Minimal reusable thread barrier (C++17).
@@ -291,7 +294,8 @@ class ThreadBarrier {
 // every rank holds `batch` pairs, negatives are global. Reports the slowest rank.
 int run_multi(const Options& o, DType in, DType comp) {
   const int N = o.gpus;
-  const std::string uid = RcclComm::unique_id();
+  const std::string uid = o.emulate ? std::string() : RcclComm::unique_id();
+  auto group = o.emulate ? make_thread_comm_group(N) : nullptr;
   ThreadBarrier bar(N);
   std::vector<double> mean_ms(N, 0.0);
   std::vector<std::string> errs(N);
@@ -301,9 +305,11 @@ int run_multi(const Options& o, DType in, DType comp) {
   for (int r = 0; r < N; ++r) {
     th.emplace_back([&, r] {
       try {
-        NTXENT_HIP_CHECK(hipSetDevice(r));
-        RcclComm comm(r, N, uid, r);
-        Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, &comm, 1234 + r);
+        NTXENT_HIP_CHECK(hipSetDevice(o.emulate ? 0 : r));
+        std::unique_ptr<Comm> comm;
+        if (o.emulate) comm = std::make_unique<ThreadComm>(group, r);
+        else comm = std::make_unique<RcclComm>(r, N, uid, r);
+        Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, comm.get(), 1234 + r, true, 0, o.negatives);
         bar.wait();
         const Result fb = stats(bench.time(o.graph ? 3 : 2, o.warmup, o.iters));
         mean_ms[r] = fb.mean;
@@ -318,8 +324,9 @@ int run_multi(const Options& o, DType in, DType comp) {
   for (int r = 0; r < N; ++r)
     if (!errs[r].empty()) { std::fprintf(stderr, "rank %d: %s\n", r, errs[r].c_str()); return 1; }
   const double ms = *std::max_element(mean_ms.begin(), mean_ms.end());
-  std::printf("gpus=%d B/gpu=%d D=%d %s: fwd+bwd %.4f ms (slowest rank), %.1f samples/s total, "
-              "%.1f TFLOP/s/GPU, loss %.6f\n", N, o.batch, o.dim, o.dtype.c_str(), ms,
+  std::printf("%s=%d B/rank=%d D=%d %s %s: fwd+bwd %.4f ms (slowest rank), %.1f samples/s total, "
+              "%.1f TFLOP/s/rank, loss %.6f\n", o.emulate ? "emulated ranks" : "gpus", N, o.batch, o.dim, o.dtype.c_str(),
+              o.negatives == Negatives::kSymmetric ? "symmetric" : "allgather", ms,
               (double)N * o.batch / (ms * 1e-3), flops / (ms * 1e-3) / 1e12, loss);
   return 0;
 }
@@ -351,14 +358,23 @@ int main(int argc, char** argv) {
     else if (a == "--no-dzsym") ntxent::set_dz_sym(false);
     else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
+    else if (a == "--no-prefetch") ntxent::set_fwd_prefetch(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
+    else if (a == "--negatives") {
+      const std::string v = next();
+      NTXENT_CHECK(v == "symmetric" || v == "allgather", "--negatives symmetric|allgather");
+      o.negatives = v == "symmetric" ? Negatives::kSymmetric : Negatives::kAllGather;
+    }
+    else if (a == "--emulate") o.emulate = true;
     else if (a == "--small-fuse-rows") ntxent::set_small_fuse_rows(std::stoi(next()));
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
                   "                    [--iters N] [--warmup W] [--temperature T] [--check] [--graph]\n"
                   "                    [--recompute] [--no-small] [--gpus N] [--json out.json]\n"
                   "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n"
+                  "  --gpus N [--negatives symmetric|allgather] [--emulate]: data parallel over N GPUs (RCCL),\n"
+                  "           or N emulated ranks on GPU 0 (in-process ThreadComm, --emulate)\n"
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"

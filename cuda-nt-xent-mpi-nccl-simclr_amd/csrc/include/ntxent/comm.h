@@ -74,6 +74,41 @@ class LocalComm final : public Comm {
   void send_recv(const std::vector<P2POp>& ops, hipStream_t stream) override;  // peer 0 only: copies
 };
 
+// In-process W-rank communicator: rank r is driven by its own host thread, all ranks in one
+// process (one GPU or several). Every collective is a host rendezvous of the W callers plus
+// device copies between their buffers, ordered on each caller's stream by events (a rank's copy
+// of a peer's buffer waits for the peer's enqueued work up to the call; every rank then waits
+// for all copies before its stream moves on), so stream semantics match RCCL's. Reductions sum
+// in rank order (deterministic). For single-GPU rehearsals of the multi-rank Engine paths and
+// their tests; RCCL refuses two ranks on one device.
+class ThreadCommGroup;
+std::shared_ptr<ThreadCommGroup> make_thread_comm_group(int world);
+class ThreadComm final : public Comm {
+ public:
+  ThreadComm(std::shared_ptr<ThreadCommGroup> group, int rank);
+  ~ThreadComm() override;
+  ThreadComm(const ThreadComm&) = delete;
+  ThreadComm& operator=(const ThreadComm&) = delete;
+
+  int rank() const override { return rank_; }
+  int world() const override;
+  void all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) override;
+  void all_reduce_sum(float* buf, size_t count, hipStream_t stream) override;
+  void reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) override;
+  void send_recv(const std::vector<P2POp>& ops, hipStream_t stream) override;
+  struct Call;  // one rank's posted collective (rccl_comm.cpp)
+
+ private:
+  template <typename Copies, typename After>
+  void collective(Call& c, hipStream_t stream, Copies&& copies, After&& after);
+  float* scratch(size_t floats);
+  std::shared_ptr<ThreadCommGroup> group_;
+  int rank_ = 0;
+  hipEvent_t ready_ = nullptr, done_ = nullptr;
+  float* scratch_ = nullptr;
+  size_t scratch_floats_ = 0;
+};
+
 // RCCL communicator (one per process / GPU).
 class RcclComm final : public Comm {
  public:

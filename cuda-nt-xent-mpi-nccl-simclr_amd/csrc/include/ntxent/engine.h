@@ -21,11 +21,21 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <utility>
+#include <vector>
 
 #include "ntxent/comm.h"
 #include "ntxent/ntxent.h"
 
 namespace ntxent {
+
+// Global-batch negatives at world > 1 (parallel/ has the same two modes on torch.distributed):
+//   kAllGather: every rank gathers all rows and computes its full row block S_{r,:};
+//   kSymmetric: every rank pair's similarity block is computed ONCE (sym_jobs): rows travel
+//     point to point in chunks (half an all-gather's bytes), the computing rank keeps row and
+//     column partials and produces the partner's gradient contribution, sent back point to point
+//     (Comm::send_recv: one grouped batch, a peer per xGMI link) while its own dZ GEMMs run.
+enum class Negatives : int { kAllGather = 0, kSymmetric = 1 };
 
 struct EngineConfig {
   int rows = 0;               // local rows R = 2 x per-view batch ([view1; view2] stacked)
@@ -52,6 +62,7 @@ struct EngineConfig {
   // world > 1: CUs the similarity GEMMs leave free while an overlapped all-gather is in flight
   // (the persistent GEMM would otherwise hold every CU and the RCCL kernels could not start)
   int comm_reserve_cus = 8;
+  Negatives negatives = Negatives::kSymmetric;  // world > 1 (kSymmetric keeps cosines)
   int device = -1;            // -1: current device
 };
 
@@ -89,6 +100,7 @@ class Engine {
   int own_tiles() const { return n_own_; }
   int dz_tiles() const { return n_dz_; }
   bool small() const { return small_; }
+  bool symmetric() const { return symm_; }
   Comm* comm() const { return comm_; }
 
  private:
@@ -104,6 +116,26 @@ class Engine {
   bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
   float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
   float* dot_ = nullptr;       // dot [Rpad]
+  // symmetric data-parallel mode (Negatives::kSymmetric, engine_sym.cpp)
+  bool symm_ = false;
+  std::vector<SymJob> jobs_, inc_;
+  int nch_ = 1, nfull_ = 0;
+  std::vector<std::pair<int, int>> segs_;  // (first, count) of each row chunk's cross tiles
+  float2* part_x_ = nullptr;               // column partials of the cross tiles
+  char* mbuf_ = nullptr;                   // partners' mirrored coefficient blocks
+  char* contrib_ = nullptr;                // partners' gradient contributions (nfull + split blocks)
+  char* recv_ = nullptr;                   // received contributions [inc][Rpad][dim_n]
+  size_t ccs_ = 2;                         // bytes per contribution element (fp16, fp32 plans: 4)
+  int4* dz_rows_ = nullptr;                // dz_view tile lists: see init_sym
+  std::vector<std::pair<int, int>> dz_ranges_;
+  std::vector<hipEvent_t> ev_chunk_;
+  hipEvent_t ev_f16_ = nullptr, ev_x_ = nullptr, ev_xdone_ = nullptr, ev_c_ = nullptr, ev_cdone_ = nullptr;
+  void init_sym();
+  void forward_sym(const void* h, hipStream_t s);
+  void backward_sym(const float* grad_out, void* dh, hipStream_t s);
+  const int4* dz_rows(int m0, int m1) const;
+  void dz_view(const char* abuf, long a_tile0, long a_panel_tiles, const char* bbuf, int b_block0, long b_col0,
+               int k_tiles, int m0, int m1, void* out, bool accum, bool out_f16, hipStream_t s);
   bool q8_ = false;            // fp8 backward (e4m3 C and Z^T, EngineConfig::fp8_backward)
   float* q8_mneg_ = nullptr;   // Q8Stats: negatives-only row max [Rpad], min LSE [1]
   float* q8_lmin_ = nullptr;

@@ -111,6 +111,12 @@ struct SymJob {
 // grouped by chunk of the partners' row tiles (chunk c = tiles [rt*c/n, rt*(c+1)/n)), each
 // segment in Z-order.
 std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJob>& jobs, int nchunks = 1);
+// The assignment itself (parallel/symmetric.py sym_jobs / sym_incoming / sym_num_chunks): the
+// blocks rank `rank` computes, and the other ranks' jobs that involve its rows (q = the
+// computing rank there). Rows travel in sym_num_chunks(row_tiles) chunks of row tiles.
+std::vector<SymJob> sym_jobs(int world, int rank, int row_tiles);
+std::vector<SymJob> sym_incoming(int world, int rank, int row_tiles);
+int sym_num_chunks(int row_tiles);
 
 // Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
 // first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered; its
@@ -157,6 +163,9 @@ size_t gemm_workspace_bytes(int ntiles, int num_cus);
 // ypos is then computed from the dequantised fp8 rows.
 void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
                  const Geometry& g, hipStream_t stream, void* zq8 = nullptr);
+
+// out[i] = sum over k = 0 .. n-1 (in order) of in[k * count + i].
+void launch_sum_slabs(const float* in, int n, size_t count, float* out, hipStream_t stream);
 
 // zqt[e][j] = zq[j][e] (zero for e >= dim_k). zqt is [dim_n][Rpad].
 void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g,
@@ -234,6 +243,9 @@ int lse_scratch_floats(const Geometry& g);
 // negatives-only max logit, log2 units), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
 // bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
 void set_fp8_backward(bool on);  // default: see ntxent_kernels.hip
+// Forward GEMM: issue the next work item's prologue DMA before the epilogue (default on; A/B)
+void set_fwd_prefetch(bool on);
+bool fwd_prefetch_enabled();
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad

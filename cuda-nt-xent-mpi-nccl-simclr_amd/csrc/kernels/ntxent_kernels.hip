@@ -416,6 +416,17 @@ __device__ __forceinline__ void transpose_tile_q8(const _Float16* __restrict__ z
   }
 }
 
+// out[i] = sum_k in[k * count + i], k = 0 .. n-1 in order (deterministic reductions of the
+// in-process communicator).
+__global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict__ in, int n, size_t count,
+                                                        float* __restrict__ out) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) {
+    float s = 0.f;
+    for (int k = 0; k < n; ++k) s += in[(size_t)k * count + i];
+    out[i] = s;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq, T* __restrict__ zqt,
                                                         int dk, int ldk, int ldt) {
@@ -725,6 +736,7 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
 
 dev::SimParams base_params(const Geometry& g) {
   dev::SimParams p{};
+  p.fwd_prefetch = fwd_prefetch_enabled() ? 1 : 0;
   p.R = g.rows;
   p.Rpad = g.rows_pad;
   p.n_half = g.rows / 2;
@@ -877,6 +889,30 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
 
 int count_own_fwd_tiles(const Geometry& g) { return g.row_tiles * (g.row_tiles + 1) / 2; }
 
+std::vector<SymJob> sym_jobs(int world, int rank, int row_tiles) {
+  std::vector<SymJob> jobs;
+  const int W = world, r = rank, rt = row_tiles;
+  for (int d = 1; d <= (W - 1) / 2; ++d) jobs.push_back(SymJob{(r + d) % W, 0, rt, 0, rt});
+  if (W % 2 == 0 && W > 1) {
+    const int q = (r + W / 2) % W, h = (rt + 1) / 2;
+    const SymJob j = r < q ? SymJob{q, 0, h, 0, rt} : SymJob{q, 0, rt, h, rt};
+    if (j.m0 < j.m1 && j.k0 < j.k1) jobs.push_back(j);
+  }
+  return jobs;
+}
+
+std::vector<SymJob> sym_incoming(int world, int rank, int row_tiles) {
+  std::vector<SymJob> out;
+  for (int p = 0; p < world; ++p) {
+    if (p == rank) continue;
+    for (const SymJob& j : sym_jobs(world, p, row_tiles))
+      if (j.q == rank) out.push_back(SymJob{p, j.m0, j.m1, j.k0, j.k1});
+  }
+  return out;
+}
+
+int sym_num_chunks(int row_tiles) { return std::max(1, std::min(4, row_tiles)); }
+
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   // Whole tiles in data-parallel rounds of G = num_cus blocks; only the remainder tiles
   // (ntiles % G) are split, into p K-pieces each, run by the first rem * p blocks after their
@@ -991,6 +1027,13 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
+void launch_sum_slabs(const float* in, int n, size_t count, float* out, hipStream_t stream) {
+  if (count == 0) return;
+  const int grid = (int)std::min<size_t>((count + 255) / 256, 1024);
+  hipLaunchKernelGGL(dev::sum_slabs_kernel, dim3(grid), dim3(256), 0, stream, in, n, count, out);
+  NTXENT_HIP_CHECK(hipGetLastError());
+}
+
 void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, hipStream_t stream) {
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
@@ -1013,6 +1056,7 @@ static std::atomic<int> g_grid_reserve{0};       // CUs the GEMMs leave free for
 static std::atomic<bool> g_dz_sym{true};         // dZ from the upper-triangular C and Zq (launch_dz_sym)
 static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
+static std::atomic<bool> g_fwd_prefetch{true};   // forward GEMM: next item's prologue under the epilogue
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1030,6 +1074,8 @@ int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
 int grid_reserve() { return g_grid_reserve.load(); }
 void set_dz_sym(bool on) { g_dz_sym = on; }
 bool dz_sym_enabled() { return g_dz_sym.load(); }
+void set_fwd_prefetch(bool on) { g_fwd_prefetch = on; }
+bool fwd_prefetch_enabled() { return g_fwd_prefetch.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }

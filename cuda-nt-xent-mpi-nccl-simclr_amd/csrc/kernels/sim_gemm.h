@@ -71,6 +71,7 @@ struct SimParams {
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
+  int fwd_prefetch;      // forward: issue the next item's prologue DMA before the epilogue
   int no_mirror;         // coefficient pass: write only the stored (upper) own-block tiles (dz_sym_kernel
                          // reads the lower ones transposed)
   // Fused normalisation backward (see dot_slots / dz_store):
@@ -711,8 +712,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // fp8: 2 KiB more hold the dwords carrying the tile's 256 A-row and 256 B-row E8M0 scales (one
   // array: a second __shared__ object makes hipcc drain the LDS-DMA before every ds_read)
   constexpr int kScaleLds = MODE == kModeCoef ? kCoefLds : kGemmLds;
-  // (+2 KiB: fp8 row scales, or the fused dZ epilogue's per-row coefficients)
-  __shared__ __attribute__((aligned(16))) char smem[kScaleLds + ((std::is_same<T, fp8e4m3>::value || MODE == kModeDz) ? 2048 : 0)];
+  // (+2 KiB: fp8 row scales, or the fused dZ epilogue's per-row coefficients; forward: + 12 KiB
+  // of row / column reductions above the stage buffers, see the prologue prefetch)
+  constexpr int kFwdRed = kScaleLds + ((std::is_same<T, fp8e4m3>::value || MODE == kModeDz) ? 2048 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[kFwdRed + (MODE == kModeFwd ? 6 * 256 * 8 : 0)];
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
@@ -879,47 +882,67 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const long long it1 = it0 + p.ipb < sk_total ? it0 + p.ipb : sk_total;
   const int n_dp = p.dp_tiles > bid ? (p.dp_tiles - bid + G - 1) / G : 0;
   long long it = it0;
-  for (int item = 0;; ++item) {
-  int tile, kb, ke, stile = -1;
-  if (item < n_dp) {
-    tile = bid + item * G;
-    kb = 0;
-    ke = nk;
-  } else {
-    if (it >= it1) break;
+  // work item `item` of this block -> (tile, K range, stream-K tile); false: no more work
+  auto fetch = [&](int item, int& tile, int& kb, int& ke, int& stile) -> bool {
+    stile = -1;
+    if (item < n_dp) {
+      tile = bid + item * G;
+      kb = 0;
+      ke = nk;
+      return true;
+    }
+    if (it >= it1) return false;
     stile = (int)(it / nk);
     kb = (int)(it % nk);
     ke = (int)((long long)kb + (it1 - it) < nk ? kb + (it1 - it) : nk);
     it += ke - kb;
     tile = p.dp_tiles + stile;
+    return true;
+  };
+  // operand streams of an item + its prologue DMA: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1
+  // (the stream clamps keep the trailing prefetches in bounds, so every wait count is uniform)
+  auto prologue = [&](int tile, int kb, int ke) {
+    const int4 tt = p.tiles[tile];
+    const int ns = ke - kb;
+    Ab = p.A.base + (long long)tt.x * p.A.row_tile_stride;
+    Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
+    const long long k0 = (long long)kb * kKStepBytes;
+    sa0.init(k0, p.A, ns); sa1.init(k0, p.A, ns);
+    sb0.init(k0, p.B, ns); sb1.init(k0, p.B, ns);
+    if constexpr (kF8 && MODE != kModeDz) {
+      // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
+      // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a
+      // 4-byte LDS-DMA issued before the half-tiles: the vmcnt(10) below retires it with A0(0), B0(0)
+      const int t = threadIdx.x;
+      const char* src = (t < 256 ? Ab + (long long)t * p.A.ld : Bb + (long long)(t - 256) * p.B.ld) + p.scale_off;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kScaleLds + 256 * w), 4, 0, 0);
+    }
+    stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
+    stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
+  };
+  // Forward: the next item's prologue is issued right after this item's stream-K fixup, so its
+  // DMA runs under the epilogue (exponentials, partial sums, cosine stores); the epilogue's LDS
+  // (row / column reductions) lives above the stage buffers for that. Younger epilogue stores
+  // only make the next item's counted waits stricter (vmcnt: all but the N youngest).
+  bool pre = false;
+  int ptile = 0, pkb = 0, pke = 0, pstile = -1;
+  for (int item = 0;; ++item) {
+  int tile, kb, ke, stile;
+  if (pre) {
+    tile = ptile; kb = pkb; ke = pke; stile = pstile;
+    pre = false;
+  } else {
+    if (!fetch(item, tile, kb, ke, stile)) break;
+    prologue(tile, kb, ke);
   }
   const int4 t = p.tiles[tile];
   const int mt = t.x, nt = t.y;
   const int nsteps = ke - kb;
-  Ab = p.A.base + (long long)mt * p.A.row_tile_stride;
-  Bb = p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride;
-  {
-    const long long k0 = (long long)kb * kKStepBytes;
-    sa0.init(k0, p.A, nsteps); sa1.init(k0, p.A, nsteps);
-    sb0.init(k0, p.B, nsteps); sb1.init(k0, p.B, nsteps);
-  }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1 (the stream clamps keep the
-  // trailing prefetches in bounds, so every wait count below is uniform)
-  if constexpr (kF8 && MODE != kModeDz) {
-    // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
-    // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a 4-byte
-    // LDS-DMA issued before the half-tiles: the vmcnt(10) below retires it with A0(0), B0(0)
-    const int t = threadIdx.x;
-    const char* src = (t < 256 ? Ab + (long long)t * p.A.ld : Bb + (long long)(t - 256) * p.B.ld) + p.scale_off;
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kScaleLds + 256 * w), 4, 0, 0);
-  }
-  stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
-  stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
   if (grp == 1) barrier();  // stagger group 1 by one barrier
@@ -987,6 +1010,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   for (int ni = 0; ni < 4; ++ni) cb[ni] = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
 
   if (nsteps != nk && !sk_fixup<kF8>(acc, p, stile, bid, G, tid, smem)) continue;
+  if constexpr (MODE == kModeFwd) {
+    if (p.fwd_prefetch && fetch(item + 1, ptile, pkb, pke, pstile)) {
+      prologue(ptile, pkb, pke);
+      pre = true;
+    }
+  }
 
   if constexpr (MODE == kModeDz) {
     if constexpr (kF8) dz8_finish(acc, p, mt, nt, rb, cb, lane);
@@ -1078,8 +1107,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       }
     }
     const float sc_ = p.acc_scale;
-    float2* rowred = reinterpret_cast<float2*>(smem);                // [4 wb][256]
-    float2* colred = reinterpret_cast<float2*>(smem + 4 * 256 * 8);  // [2 wa][256]
+    float2* rowred = reinterpret_cast<float2*>(smem + kFwdRed);                // [4 wb][256]
+    float2* colred = reinterpret_cast<float2*>(smem + kFwdRed + 4 * 256 * 8);  // [2 wa][256]
     if constexpr (fixed) {
       // Streamed per 16-row block: exponentiate (exp2(-inf) = 0 for the masked elements),
       // reduce the 4 rows, fold into the column sums; acc[mi] is dead afterwards, which keeps

@@ -39,14 +39,24 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   bwd_ = backward_dtype(cfg.compute);
   cs_ = dtype_size(bwd_);
   small_ = cfg.small_path && world_ == 1 && small_path_eligible(g_, cfg.compute);
+  symm_ = world_ > 1 && cfg.negatives == Negatives::kSymmetric;
+  if (symm_) {
+    cfg_.keep_cos = true;  // the coefficient pass reads both blocks' cosines from the forward
+    jobs_ = sym_jobs(world_, rank_, g_.row_tiles);
+    inc_ = sym_incoming(world_, rank_, g_.row_tiles);
+    nch_ = sym_num_chunks(g_.row_tiles);
+    ccs_ = bwd_ == DType::F32 ? 4 : 2;
+  }
   // dZ straight from the upper-triangular C and the (gathered) Zq rows: no ZqT, no mirrors
   q8_ = !small_ && fp8_backward_eligible(g_, cfg.compute) &&
         (cfg.fp8_backward < 0 ? fp8_backward_enabled() : cfg.fp8_backward != 0);
-  sym_ = !small_ && !q8_ && cfg.dz_sym && dz_sym_enabled() && dz_sym_eligible(g_, cfg.compute);
-  // normalisation backward fused into the dZ epilogue (the coefficient pass emits dot partials)
-  fuse_ = !small_ && bwd_ != DType::F32 && norm_fuse_enabled() && g_.dim % 8 == 0;
+  sym_ = !small_ && !q8_ && !symm_ && cfg.dz_sym && dz_sym_enabled() && dz_sym_eligible(g_, cfg.compute);
+  // normalisation backward fused into the dZ epilogue (the coefficient pass emits dot partials;
+  // the symmetric mode sums received contributions in launch_norm_bwd instead)
+  // (not on fp8 plans: dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines, ~1e-2 off)
+  fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && norm_fuse_enabled() && g_.dim % 8 == 0;
 
-  const auto ft = build_fwd_tiles(g_);
+  const auto ft = symm_ ? build_sym_fwd_tiles(g_, jobs_, nch_) : build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
   n_fwd_ = (int)ft.size();
   n_own_ = count_own_fwd_tiles(g_);
@@ -73,7 +83,13 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&block_loss_, (size_t)lse_scratch_floats(g_) * 4},
       {(void**)&loss_, 4},
       {(void**)&one_, 4},
-      {(void**)&slabs_, Rp * g_.dim_n * 4},
+      // symmetric mode, fp32 plans: the received contributions follow the own slab (one stack)
+      {(void**)&slabs_, Rp * g_.dim_n * 4 * (symm_ && ccs_ == 4 ? 1 + inc_.size() : 1)},
+      {(void**)&part_x_, symm_ ? (size_t)g_.col_tiles * Rp * sizeof(float2) : 0},
+      {(void**)&mbuf_, symm_ ? (size_t)std::max(1, world_ / 2) * g_.row_tiles * g_.row_tiles * kTileElems * cs_ : 0},
+      {(void**)&contrib_, symm_ ? (jobs_.size() + 1) * Rp * g_.dim_n * ccs_ : 0},
+      {(void**)&recv_, symm_ && ccs_ == 2 ? inc_.size() * Rp * g_.dim_n * ccs_ : 0},
+      {(void**)&dz_rows_, symm_ ? (size_t)4 * (world_ + 1) * g_.row_tiles * (g_.dim_n / kTile) * sizeof(int4) : 0},
       {(void**)&dotp_, fuse_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
       {(void**)&dot_, fuse_ ? Rp * 4 : 0},
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
@@ -104,9 +120,13 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev_zq_, hipEventDisableTiming));
     NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ev_zqt_, hipEventDisableTiming));
   }
+  if (symm_) init_sym();
 }
 
 Engine::~Engine() {
+  for (hipEvent_t e : ev_chunk_) hipEventDestroy(e);
+  for (hipEvent_t e : {ev_f16_, ev_x_, ev_xdone_, ev_c_, ev_cdone_})
+    if (e) hipEventDestroy(e);
   if (exec_) hipGraphExecDestroy(exec_);
   if (graph_) hipGraphDestroy(graph_);
   if (ev_prep_) hipEventDestroy(ev_prep_);
@@ -119,6 +139,10 @@ Engine::~Engine() {
 void Engine::forward(const void* h, hipStream_t s) {
   NTXENT_TRACE("ntxent.forward");
   h_ = h;
+  if (symm_) {
+    forward_sym(h, s);
+    return;
+  }
   const size_t Rp = g_.rows_pad;
   char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
   char* zqt_local = zqt_all_ + (size_t)rank_ * g_.dim_n * g_.ld_t * cs_;
@@ -196,6 +220,10 @@ void Engine::forward(const void* h, hipStream_t s) {
 void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   NTXENT_TRACE("ntxent.backward");
   NTXENT_CHECK(h_ != nullptr, "backward() before forward()");
+  if (symm_) {
+    backward_sym(grad_out, dh, s);
+    return;
+  }
   const size_t Rp = g_.rows_pad;
   const char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
   Q8Stats q8;  // fp8 backward (q8_)

@@ -690,7 +690,9 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     q8.zq = zq.data_ptr();
     NTXENT_CHECK(sc_in.has_value() && sc_in->defined() && cpos.numel() == 2 * Rp + 64,
                  "fused_backward (fp8): kept cosines and the forward's Q8Stats required");
-    const bool fuse = norm_fuse_enabled();
+    // (no fused normalisation backward on fp8 plans: its dot_i = sum_j C_ij cos_ij would use the
+    // e4m3 forward's cosines instead of z_i . g_i, a ~1e-2 radial error in dh)
+    const bool fuse = false;
     at::Tensor dotp, dot, dh, go;
     if (fuse) {
       dotp = at::empty({Rp * dot_slots(P->g)}, opts(h, at::kFloat));
@@ -723,7 +725,8 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   const bool sym = zqt.numel() == 0;  // dz_sym forward (see fused_forward)
   // dz_sym plans finish the normalisation backward in the dZ epilogue (norm_fuse_enabled): the
   // coefficient pass also emits the partials of dot_i = z_i . g_i
-  const bool fuse = P->bwd() != DType::F32 && norm_fuse_enabled() && P->g.dim % 8 == 0;
+  // (not on fp8 plans: the fused dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines)
+  const bool fuse = P->bwd() != DType::F32 && P->comp != DType::FP8 && norm_fuse_enabled() && P->g.dim % 8 == 0;
   at::Tensor dotp, dot;
   if (fuse) {
     dotp = at::empty({(long)P->g.rows_pad * dot_slots(P->g)}, opts(h, at::kFloat));
@@ -953,6 +956,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_dz_sym", &ntxent::set_dz_sym, py::arg("on"));
   m.def("set_norm_fuse", &ntxent::set_norm_fuse, py::arg("on"));
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
+  m.def("set_fwd_prefetch", &ntxent::set_fwd_prefetch, py::arg("on"));
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
   m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);

@@ -2,7 +2,9 @@
 #include "ntxent/comm.h"
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 
@@ -32,6 +34,159 @@ void LocalComm::send_recv(const std::vector<P2POp>& ops, hipStream_t stream) {
     if (sends[k]->bytes && sends[k]->buf != recvs[k]->buf)
       NTXENT_HIP_CHECK(hipMemcpyAsync(recvs[k]->buf, sends[k]->buf, sends[k]->bytes, hipMemcpyDeviceToDevice, stream));
   }
+}
+
+// ---- ThreadComm ---------------------------------------------------------------------------
+struct ThreadComm::Call {
+  const void* send = nullptr;
+  void* recv = nullptr;
+  size_t bytes = 0;
+  const std::vector<P2POp>* ops = nullptr;
+  hipEvent_t ready = nullptr, done = nullptr;
+};
+
+class ThreadCommGroup {
+ public:
+  explicit ThreadCommGroup(int world) : world_(world), calls_(world) {}
+  int world() const { return world_; }
+  // host rendezvous of the W callers (generation counted, reusable)
+  void barrier() {
+    std::unique_lock<std::mutex> l(m_);
+    const long gen = gen_;
+    if (++arrived_ == world_) {
+      arrived_ = 0;
+      ++gen_;
+      cv_.notify_all();
+    } else {
+      cv_.wait(l, [&] { return gen != gen_; });
+    }
+  }
+  std::vector<ThreadComm::Call*>& calls() { return calls_; }
+
+ private:
+  int world_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  long gen_ = 0;
+  std::vector<ThreadComm::Call*> calls_;
+};
+
+std::shared_ptr<ThreadCommGroup> make_thread_comm_group(int world) {
+  NTXENT_CHECK(world >= 1, "thread comm: world must be >= 1");
+  return std::make_shared<ThreadCommGroup>(world);
+}
+
+ThreadComm::ThreadComm(std::shared_ptr<ThreadCommGroup> group, int rank) : group_(std::move(group)), rank_(rank) {
+  NTXENT_CHECK(group_ && rank >= 0 && rank < group_->world(), "ThreadComm: bad rank");
+  NTXENT_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  NTXENT_HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+}
+
+ThreadComm::~ThreadComm() {
+  if (ready_) hipEventDestroy(ready_);
+  if (done_) hipEventDestroy(done_);
+  if (scratch_) hipFree(scratch_);
+}
+
+int ThreadComm::world() const { return group_->world(); }
+
+float* ThreadComm::scratch(size_t floats) {
+  if (floats > scratch_floats_) {
+    // (the device is idle for this rank's buffers: a reduction's scratch is only read by its own
+    // stream after the rendezvous)
+    if (scratch_) NTXENT_HIP_CHECK(hipFree(scratch_));
+    NTXENT_HIP_CHECK(hipMalloc(&scratch_, floats * sizeof(float)));
+    scratch_floats_ = floats;
+  }
+  return scratch_;
+}
+
+// 1. mark this rank's enqueued work (ready), publish the call; rendezvous
+// 2. enqueue the copies out of the peers' buffers (each after that peer's ready event); mark done
+// 3. rendezvous; wait for every peer's copies (done) -> the peers' buffers may change again
+// 4. `after` (the reduction, once every copy has landed); rendezvous so that no rank re-records
+//    its events before every peer has enqueued its waits on them
+template <typename Copies, typename After>
+void ThreadComm::collective(Call& c, hipStream_t stream, Copies&& copies, After&& after) {
+  auto& calls = group_->calls();
+  NTXENT_HIP_CHECK(hipEventRecord(ready_, stream));
+  c.ready = ready_;
+  c.done = done_;
+  calls[rank_] = &c;
+  group_->barrier();
+  copies(calls);
+  NTXENT_HIP_CHECK(hipEventRecord(done_, stream));
+  group_->barrier();
+  for (int q = 0; q < world(); ++q)
+    if (q != rank_) NTXENT_HIP_CHECK(hipStreamWaitEvent(stream, calls[q]->done, 0));
+  after();
+  group_->barrier();
+}
+
+void ThreadComm::all_gather(const void* send, void* recv, size_t bytes, hipStream_t stream) {
+  Call c;
+  c.send = send;
+  collective(c, stream, [&](std::vector<Call*>& calls) {
+    char* out = static_cast<char*>(recv);
+    for (int q = 0; q < world(); ++q) {
+      char* dst = out + (size_t)q * bytes;
+      if (calls[q]->send == dst || bytes == 0) continue;
+      if (q != rank_) NTXENT_HIP_CHECK(hipStreamWaitEvent(stream, calls[q]->ready, 0));
+      NTXENT_HIP_CHECK(hipMemcpyAsync(dst, calls[q]->send, bytes, hipMemcpyDeviceToDevice, stream));
+    }
+  }, [] {});
+}
+
+void ThreadComm::all_reduce_sum(float* buf, size_t count, hipStream_t stream) {
+  Call c;
+  c.send = buf;
+  const int W = world();
+  float* tmp = scratch((size_t)W * count);
+  collective(c, stream, [&](std::vector<Call*>& calls) {
+    for (int q = 0; q < W; ++q) {
+      if (q != rank_) NTXENT_HIP_CHECK(hipStreamWaitEvent(stream, calls[q]->ready, 0));
+      NTXENT_HIP_CHECK(hipMemcpyAsync(tmp + (size_t)q * count, calls[q]->send, count * sizeof(float),
+                                      hipMemcpyDeviceToDevice, stream));
+    }
+  }, [&] { launch_sum_slabs(tmp, W, count, buf, stream); });
+}
+
+void ThreadComm::reduce_scatter_sum(const float* send, float* recv, size_t count, hipStream_t stream) {
+  Call c;
+  c.send = send;
+  const int W = world();
+  float* tmp = scratch((size_t)W * count);
+  collective(c, stream, [&](std::vector<Call*>& calls) {
+    for (int q = 0; q < W; ++q) {
+      if (q != rank_) NTXENT_HIP_CHECK(hipStreamWaitEvent(stream, calls[q]->ready, 0));
+      NTXENT_HIP_CHECK(hipMemcpyAsync(tmp + (size_t)q * count,
+                                      static_cast<const float*>(calls[q]->send) + (size_t)rank_ * count,
+                                      count * sizeof(float), hipMemcpyDeviceToDevice, stream));
+    }
+  }, [&] { launch_sum_slabs(tmp, W, count, recv, stream); });
+}
+
+void ThreadComm::send_recv(const std::vector<P2POp>& ops, hipStream_t stream) {
+  Call c;
+  c.ops = &ops;
+  collective(c, stream, [&](std::vector<Call*>& calls) {
+    // the k-th receive from q matches q's k-th send to this rank
+    std::vector<int> seen(world(), 0);
+    for (const auto& o : ops) {
+      NTXENT_CHECK(o.peer >= 0 && o.peer < world(), "ThreadComm::send_recv: peer out of range");
+      if (o.send) continue;
+      const int q = o.peer, k = seen[q]++;
+      const P2POp* match = nullptr;
+      int n = 0;
+      for (const auto& so : *calls[q]->ops)
+        if (so.send && so.peer == rank_ && n++ == k) { match = &so; break; }
+      NTXENT_CHECK(match != nullptr && match->bytes == o.bytes, "ThreadComm::send_recv: unmatched transfer");
+      if (o.bytes == 0) continue;
+      if (q != rank_) NTXENT_HIP_CHECK(hipStreamWaitEvent(stream, calls[q]->ready, 0));
+      NTXENT_HIP_CHECK(hipMemcpyAsync(o.buf, match->buf, o.bytes, hipMemcpyDeviceToDevice, stream));
+    }
+  }, [] {});
 }
 
 void Comm::all_gather_chunks(const void* send, void* recv, size_t bytes, int nchunks, hipStream_t stream,

@@ -19,6 +19,7 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ntxent/comm.h"
@@ -127,6 +128,55 @@ void oracle(const std::vector<float>& h, int R, int d, double T, double go, doub
   }
 }
 
+// Data-parallel oracle: W ranks of R rows each (rank r's rows are global rows r*R .. r*R+R-1,
+// its positives pair within the rank: i <-> i + R/2), negatives over all W*R rows; the loss is
+// the global mean (what every rank's Engine reports) and dh the gradient of the global loss.
+void oracle_dp(const std::vector<float>& h, int W, int R, int d, double T, double& loss, std::vector<double>& dh) {
+  const int N = W * R, n = R / 2;
+  auto pos = [&](int g) { return (g / R) * R + (g % R + n) % R; };
+  std::vector<double> z((size_t)N * d), inv(N);
+  for (int i = 0; i < N; ++i) {
+    double ss = 0;
+    for (int e = 0; e < d; ++e) ss += (double)h[(size_t)i * d + e] * h[(size_t)i * d + e];
+    inv[i] = 1.0 / std::max(std::sqrt(ss), 1e-12);
+    for (int e = 0; e < d; ++e) z[(size_t)i * d + e] = h[(size_t)i * d + e] * inv[i];
+  }
+  std::vector<double> S((size_t)N * N), lse(N);
+  loss = 0;
+  for (int i = 0; i < N; ++i) {
+    double mx = -1e300;
+    for (int j = 0; j < N; ++j) {
+      double s = 0;
+      for (int e = 0; e < d; ++e) s += z[(size_t)i * d + e] * z[(size_t)j * d + e];
+      S[(size_t)i * N + j] = s / T;
+      if (j != i) mx = std::max(mx, s / T);
+    }
+    double se = 0;
+    for (int j = 0; j < N; ++j)
+      if (j != i) se += std::exp(S[(size_t)i * N + j] - mx);
+    lse[i] = mx + std::log(se);
+    loss += lse[i] - S[(size_t)i * N + pos(i)];
+  }
+  loss /= N;
+  dh.assign((size_t)N * d, 0.0);
+  std::vector<double> dz(d);
+  for (int i = 0; i < N; ++i) {
+    std::fill(dz.begin(), dz.end(), 0.0);
+    for (int j = 0; j < N; ++j) {
+      if (j == i) continue;
+      double c = std::exp(S[(size_t)i * N + j] - lse[i]) + std::exp(S[(size_t)j * N + i] - lse[j]);
+      if (j == pos(i)) c -= 2.0;
+      for (int e = 0; e < d; ++e) dz[e] += c * z[(size_t)j * d + e];
+    }
+    double dot = 0;
+    for (int e = 0; e < d; ++e) {
+      dz[e] /= N * T;
+      dot += z[(size_t)i * d + e] * dz[e];
+    }
+    for (int e = 0; e < d; ++e) dh[(size_t)i * d + e] = inv[i] * (dz[e] - z[(size_t)i * d + e] * dot);
+  }
+}
+
 // One engine run on device data; returns loss and dh (as float).
 struct Run {
   float loss = 0;
@@ -136,9 +186,10 @@ struct Run {
 class Harness {
  public:
   Harness(std::vector<float> h, int R, int d, DType in, DType comp, float T, bool keep = true, Comm* comm = nullptr,
-          bool check_finite = false)
+          bool check_finite = false, Negatives neg = Negatives::kSymmetric)
       : host_(std::move(h)), R_(R), d_(d), in_(in) {
     EngineConfig c;
+    c.negatives = neg;
     c.rows = R;
     c.dim = d;
     c.temperature = T;
@@ -418,6 +469,70 @@ NT_TEST(RcclCommPrimitivesWorldOne) {
   RcclComm comm(0, 1, RcclComm::unique_id(), 0);
   comm_primitives(comm, "RcclComm");
   comm.check();
+}
+
+// The multi-rank Engine paths (all-gather and symmetric negatives) on ONE GPU: W emulated ranks,
+// one host thread each, over the in-process ThreadComm (RCCL refuses two ranks on a device);
+// every rank's loss and gradient against the data-parallel fp64 oracle.
+static void multi_rank_case(int W, int R, int d, DType comp, Negatives neg, double loss_tol, double grad_tol) {
+  const auto h = embeddings(W * R, d, 100 + W * 7 + (int)neg);
+  auto group = make_thread_comm_group(W);
+  std::vector<std::unique_ptr<ThreadComm>> comms;
+  for (int r = 0; r < W; ++r) comms.push_back(std::make_unique<ThreadComm>(group, r));
+  std::vector<std::unique_ptr<Harness>> hs(W);
+  for (int r = 0; r < W; ++r)
+    hs[r] = std::make_unique<Harness>(std::vector<float>(h.begin() + (size_t)r * R * d, h.begin() + (size_t)(r + 1) * R * d),
+                                      R, d, comp == DType::F32 ? DType::F32 : DType::BF16, comp, kT, true,
+                                      comms[r].get(), false, neg);
+  EXPECT(W == 1 || hs[0]->engine().symmetric() == (neg == Negatives::kSymmetric), "mode not selected");
+  std::vector<Run> runs(W);
+  std::vector<std::string> errs(W);
+  std::vector<std::thread> th;
+  for (int r = 0; r < W; ++r)
+    th.emplace_back([&, r] {
+      try {
+        NTXENT_HIP_CHECK(hipSetDevice(0));
+        for (int it = 0; it < 2; ++it) runs[r] = hs[r]->run();  // twice: reusable events / buffers
+      } catch (const std::exception& e) {
+        errs[r] = e.what();
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < W; ++r) EXPECT(errs[r].empty(), "rank %d: %s", r, errs[r].c_str());
+  std::vector<float> host;
+  for (int r = 0; r < W; ++r) host.insert(host.end(), hs[r]->host().begin(), hs[r]->host().end());
+  double lref;
+  std::vector<double> gref;
+  oracle_dp(host, W, R, d, kT, lref, gref);
+  std::vector<float> dh;
+  for (int r = 0; r < W; ++r) {
+    EXPECT(std::fabs(runs[r].loss - lref) <= loss_tol * std::fabs(lref), "W=%d rank %d loss %.7f ref %.7f", W, r,
+           runs[r].loss, lref);
+    dh.insert(dh.end(), runs[r].dh.begin(), runs[r].dh.end());
+  }
+  const double gr = rel_l2(dh, gref);
+  EXPECT(gr <= grad_tol, "W=%d %s grad rel err %.3e > %.1e", W, neg == Negatives::kSymmetric ? "symmetric" : "allgather",
+         gr, grad_tol);
+  std::printf("         W=%d %-9s loss %.6f (oracle %.6f) grad rel err %.2e\n", W,
+              neg == Negatives::kSymmetric ? "symmetric" : "allgather", runs[0].loss, lref, gr);
+}
+
+NT_TEST(ThreadCommPrimitives) {  // world 1 semantics of the in-process communicator
+  auto g = make_thread_comm_group(1);
+  ThreadComm c(g, 0);
+  comm_primitives(c, "ThreadComm");
+}
+
+NT_TEST(MultiRankSymmetric) {
+  for (int W : {2, 3, 4}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kSymmetric, 2e-3, 2e-2);
+}
+
+NT_TEST(MultiRankAllGather) {
+  for (int W : {2, 3}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kAllGather, 2e-3, 2e-2);
+}
+
+NT_TEST(MultiRankSymmetricFp32) {  // fp32 contributions on the wire, one slab stack
+  multi_rank_case(3, 512, 96, DType::F32, Negatives::kSymmetric, 1e-5, 1e-4);
 }
 
 NT_TEST(FaultInjection) {

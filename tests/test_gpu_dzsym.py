@@ -75,7 +75,8 @@ def test_dz_sym_native_raw_backward(ext):
     (4096, 512, "fp16", True, True),
     (3000, 256, "bf16", True, True),     # padded rows: the fused epilogue's row guard
     (2048, 1024, "fp16", False, True),   # coefficient-GEMM flow (dot partials in the recompute epilogue)
-    (2560, 512, "fp8", True, False),     # launch_dz path (no dz_sym) with the fused epilogue
+    (2560, 512, "fp16", True, False),    # launch_dz path (no dz_sym) with the fused epilogue
+    (2560, 512, "fp8", True, False),     # fp8 plans: never fused (bitwise the unfused result)
     (4096, 520, "bf16", True, True),     # d % 256 != 0: partial last column tile
     (8192, 1024, "fp16", True, True),    # enough dZ tiles for whole-tile rounds (epilogue, not split-K reduce)
 ])
@@ -98,6 +99,8 @@ def test_norm_fuse_matches_unfused(ext, rows, dim, compute, keep, sym):
     scale = g0.abs().max().item()
     diff = (g1 - g0).abs().max().item()
     print(f"NORMFUSE rows={rows} dim={dim} compute={compute} keep={keep} sym={sym} rel diff={diff / scale:.3e}")
+    if compute == "fp8":
+        assert torch.equal(g1, g0)
     assert diff <= (1e-2 if compute == "bf16" else 2e-3) * scale
     if compute != "fp8" and rows * rows * dim <= 2 ** 34:  # (host fp64 oracle)
         lref, gref = _oracle(hb.float(), 0.1)

@@ -29,7 +29,7 @@ ARCH = os.environ.get("NTXENT_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
-RUNTIME_SRCS = ["engine.cpp", "rccl_comm.cpp", "trace.cpp"]
+RUNTIME_SRCS = ["engine.cpp", "engine_sym.cpp", "rccl_comm.cpp", "trace.cpp"]
 KERNEL_SRCS = [CSRC / "kernels" / "ntxent_kernels.hip", CSRC / "kernels" / "small_kernels.hip"]
 
 

@@ -7,8 +7,9 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3}; mkdir -p $OUT
 FIRST=${2:-}
-timeout -k 10 300 build/bin/ntxent_tests > $OUT/cpp_tests.log 2>&1 || { echo "cpp tests failed"; tail -30 $OUT/cpp_tests.log; exit 1; }
-tail -1 $OUT/cpp_tests.log
+timeout -k 10 300 build/bin/ntxent_tests > $OUT/cpp_tests.log 2>&1
+rc=$?; [ $rc -eq 0 ] || { echo "cpp tests failed rc=$rc"; grep -E "FAIL|W=" $OUT/cpp_tests.log | head -20; [ $rc -ge 124 ] && exit 1; }
+grep -E "W=|passed" $OUT/cpp_tests.log | tail -12
 if [ -n "$FIRST" ]; then
   timeout -k 10 400 python -u -m pytest $FIRST -x -v -s --timeout 120 --timeout-method thread > $OUT/pytest_first.log 2>&1 || { echo "first tests failed"; tail -40 $OUT/pytest_first.log; exit 1; }
   grep -E "DZSYM|passed|failed" $OUT/pytest_first.log | tail -12
