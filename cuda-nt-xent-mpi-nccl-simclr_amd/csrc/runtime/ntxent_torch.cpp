@@ -267,7 +267,7 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
   check_input(part, "part");
   NTXENT_CHECK(lse2_all.numel() == (long)P.g.world * P.g.rows_pad && lse2_all.scalar_type() == at::kFloat,
                "lse2_all must be float32 [world*rows_pad]");
-  NTXENT_CHECK(cpos.numel() == P.g.rows_pad && cpos.scalar_type() == at::kFloat, "cpos must be float32 [rows_pad]");
+  NTXENT_CHECK(cpos.numel() >= P.g.rows_pad && cpos.scalar_type() == at::kFloat, "cpos must be float32 [>= rows_pad]");
   const at::DeviceGuard guard(part.device());
   auto block_loss = device_scratch(part, (size_t)lse_scratch_floats(P.g) * 4, 1);
   auto loss = at::empty({}, opts(part, at::kFloat));
@@ -660,7 +660,8 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
                cur_stream(h), DType::F16, pr[0].data_ptr(), nullptr, &q8);
     return {loss, pr[0], zq8t, pr[1], lse2, fs[1], cpos};
   }
-  auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+  // (fp8 plans: 64 spare entries mark the e4m3 forward for the backward, which sees the fp16 rows)
+  auto cpos = at::empty({P->g.rows_pad + (f8 ? 64 : 0)}, opts(h, at::kFloat));
   auto loss = sym ? lse(fs[0], pr[2], lse2, cpos, *P) : lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
@@ -726,7 +727,8 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   // dz_sym plans finish the normalisation backward in the dZ epilogue (norm_fuse_enabled): the
   // coefficient pass also emits the partials of dot_i = z_i . g_i
   // (not on fp8 plans: the fused dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines)
-  const bool fuse = P->bwd() != DType::F32 && P->comp != DType::FP8 && norm_fuse_enabled() && P->g.dim % 8 == 0;
+  const bool f8_fwd = cpos.numel() != P->g.rows_pad;  // see fused_forward
+  const bool fuse = P->bwd() != DType::F32 && !f8_fwd && norm_fuse_enabled() && P->g.dim % 8 == 0;
   at::Tensor dotp, dot;
   if (fuse) {
     dotp = at::empty({(long)P->g.rows_pad * dot_slots(P->g)}, opts(h, at::kFloat));
