@@ -356,6 +356,8 @@ int main(int argc, char** argv) {
     else if (a == "--no-subtiles") ntxent::set_diag_subtiles(false);
     else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
     else if (a == "--no-dzsym") ntxent::set_dz_sym(false);
+    else if (a == "--dzsym") ntxent::set_dz_sym(true);
+    else if (a == "--prefetch") ntxent::set_fwd_prefetch(true);
     else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
     else if (a == "--no-prefetch") ntxent::set_fwd_prefetch(false);
@@ -379,8 +381,9 @@ int main(int argc, char** argv) {
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"
                   "  --no-strips: forward remainder tiles by the stream-K split instead of diagonal strips (A/B)\n"
-                  "  --no-dzsym: backward through mirrored coefficient tiles + ZqT + launch_dz (A/B against the\n"
-                  "              default upper-triangular C + Zq dZ GEMM)\n");
+                  "  --dzsym / --no-dzsym: backward from the upper-triangular C + Zq (launch_dz_sym), or through\n"
+                  "              mirrored coefficient tiles + ZqT + launch_dz (default)\n"
+                  "  --prefetch: forward GEMM issues the next item's prologue under the epilogue (A/B)\n");
       return 0;
     }
   }

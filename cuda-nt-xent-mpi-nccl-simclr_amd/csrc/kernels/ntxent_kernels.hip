@@ -676,19 +676,21 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
 }
 
 // dot_i = sum over the coefficient pass's slots of dotp[i][.] (fixed order: deterministic).
+// 16 lanes per row (coalesced 16-B loads, slots 4l + 64k for lane l), a row16 DPP sum; 16 rows
+// per block (a thread per row left the launch ~6 us at the headline: 32 blocks, each load
+// instruction touching 64 rows).
 __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict__ dotp, int nslot, int rows,
                                                          float* __restrict__ dot) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= rows) return;
-  const float* r = dotp + (long long)i * nslot;
+  const int i = blockIdx.x * 16 + (threadIdx.x >> 4), l = threadIdx.x & 15;
+  const float* r = dotp + (long long)(i < rows ? i : 0) * nslot;
   float s = 0.f;
-  int k = 0;
-  for (; k + 4 <= nslot; k += 4) {
+  for (int k = 4 * l; k + 4 <= nslot; k += 64) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
     s += (v[0] + v[1]) + (v[2] + v[3]);
   }
-  for (; k < nslot; ++k) s += r[k];
-  dot[i] = s;
+  for (int k = (nslot & ~3) + l; k < nslot; k += 16) s += r[k];  // (nslot is a multiple of 4 here)
+  s = row16_sum(s);
+  if (l == 0 && i < rows) dot[i] = s;
 }
 
 }  // namespace dev
@@ -1053,10 +1055,12 @@ static std::atomic<bool> g_small_path{true};     // one-launch small-problem for
 static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
 static std::atomic<int> g_small_fuse_rows{-1};   // small forward: fused row prologue up to R rows (-1: default)
 static std::atomic<int> g_grid_reserve{0};       // CUs the GEMMs leave free for overlapped RCCL kernels
-static std::atomic<bool> g_dz_sym{true};         // dZ from the upper-triangular C and Zq (launch_dz_sym)
+static std::atomic<bool> g_dz_sym{false};        // dZ from the upper-triangular C and Zq (launch_dz_sym): A/B
+                                                 // (profiles/r3/ab: its GEMM is slower than coef mirrors + ZqT save)
 static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
-static std::atomic<bool> g_fwd_prefetch{true};   // forward GEMM: next item's prologue under the epilogue
+static std::atomic<bool> g_fwd_prefetch{false};  // forward GEMM: next item's prologue under the epilogue (A/B:
+                                                 // no gain measured, profiles/r3/ab)
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1276,7 +1280,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 int dot_slots(const Geometry& g) { return 4 * g.col_tiles; }
 
 void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream) {
-  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 255) / 256), dim3(256), 0, stream, dotp, dot_slots(g),
+  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 15) / 16), dim3(256), 0, stream, dotp, dot_slots(g),
                      g.rows_pad, dot);
   NTXENT_HIP_CHECK(hipGetLastError());
 }
