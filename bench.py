@@ -56,6 +56,10 @@ def parse(argv=None):
     ap.add_argument("--temperature", type=float, default=0.07)
     ap.add_argument("--recompute", action="store_true", help="recompute logits in backward")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--compute-stream", default="high", choices=["default", "new", "high"],
+                    help="stream the step runs on: the device's default stream, a new stream, or a new "
+                         "high-priority stream (default; RCCL kernels then run beside the GEMMs instead of "
+                         "queueing behind them on a shared hardware queue, profiles/r3/overlap)")
     ap.add_argument("--negatives", default="symmetric", choices=["allgather", "symmetric", "ring"],
                     help="N>1: symmetric = each rank pair's similarity block computed once (column partials and "
                          "partner gradient contributions exchanged point to point); allgather = every rank computes "
@@ -202,6 +206,12 @@ def run_rank(a) -> None:
         world_seen = dist.get_world_size()
         if world_seen != world:
             raise SystemExit(f"process group has {world_seen} ranks, expected {world}")
+    if on_gpu and a.compute_stream != "default":
+        # A non-default compute stream: on the default stream the RCCL kernels of the overlapped
+        # transfers shared a hardware queue with the GEMMs and ran only between them (1-2 % of a
+        # transfer hidden under the forward GEMM vs 13-18 % on a new or high-priority stream,
+        # tools/overlap_proxy.py, profiles/r3/overlap).
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1 if a.compute_stream == "high" else 0))
     if os.environ.get("NTXENT_BENCH_FAIL_RANK") == str(rank):  # fault injection (launcher tests)
         raise SystemExit(3)
 
@@ -388,6 +398,7 @@ def run_rank(a) -> None:
                 "negatives": a.negatives if world > 1 else None,
                 "backend": backend if world > 1 else None,
                 "hip_graph": bool(a.graph),
+                "compute_stream": a.compute_stream if on_gpu else None,
                 "device": a.device,
             },
             "prewarm_steps": prewarm,
