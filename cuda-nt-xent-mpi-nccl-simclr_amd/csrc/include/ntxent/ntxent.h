@@ -269,7 +269,7 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 // multiplies this rank's rows in rank q's gradient; consecutive slots stack into one tall A.
 // upper_only: write only the tiles of `tiles` themselves (no mirrored lower own-block tiles): the
 // layout launch_dz_sym reads.
-// dotp (optional, [Rpad][dot_slots(g)] floats): partials of dot_i = sum_j C_ij cos_ij, the
+// dotp (optional, [dot_slots(g)][Rpad] floats, slot-major): partials of dot_i = sum_j C_ij cos_ij, the
 // z_i . g_i of the normalisation backward, for the fused dZ epilogue (NormFuse); every slot is
 // written (all-gather layout, own-block tiles + remote tiles of the plan).
 int dot_slots(const Geometry& g);

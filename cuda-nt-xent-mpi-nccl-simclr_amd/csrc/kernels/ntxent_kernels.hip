@@ -675,22 +675,28 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
   }
 }
 
-// dot_i = sum over the coefficient pass's slots of dotp[i][.] (fixed order: deterministic).
-// 16 lanes per row (coalesced 16-B loads, slots 4l + 64k for lane l), a row16 DPP sum; 16 rows
-// per block (a thread per row left the launch ~6 us at the headline: 32 blocks, each load
-// instruction touching 64 rows).
+// dot_i = sum over the coefficient pass's slots dotp[k][i] (slot-major; fixed order: deterministic).
+// 4 threads per row (slots q, q + 4, ...; 8 loads in flight each), 64 rows per block: the loads
+// of a wave cover 16 consecutive rows of 4 slots.
 __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict__ dotp, int nslot, int rows,
                                                          float* __restrict__ dot) {
-  const int i = blockIdx.x * 16 + (threadIdx.x >> 4), l = threadIdx.x & 15;
-  const float* r = dotp + (long long)(i < rows ? i : 0) * nslot;
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  __shared__ float part[4][64];
   float s = 0.f;
-  for (int k = 4 * l; k + 4 <= nslot; k += 64) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(r + k);
-    s += (v[0] + v[1]) + (v[2] + v[3]);
+  if (i < rows) {
+    int k = q;
+    for (; k + 28 < nslot; k += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = dotp[(long long)(k + 4 * u) * rows + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < nslot; k += 4) s += dotp[(long long)k * rows + i];
   }
-  for (int k = (nslot & ~3) + l; k < nslot; k += 16) s += r[k];  // (nslot is a multiple of 4 here)
-  s = row16_sum(s);
-  if (l == 0 && i < rows) dot[i] = s;
+  part[q][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (q == 0 && i < rows) dot[i] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
 }  // namespace dev
@@ -1280,7 +1286,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 int dot_slots(const Geometry& g) { return 4 * g.col_tiles; }
 
 void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream) {
-  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 15) / 16), dim3(256), 0, stream, dotp, dot_slots(g),
+  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 63) / 64), dim3(256), 0, stream, dotp, dot_slots(g),
                      g.rows_pad, dot);
   NTXENT_HIP_CHECK(hipGetLastError());
 }

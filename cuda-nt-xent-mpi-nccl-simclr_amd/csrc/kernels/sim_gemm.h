@@ -75,7 +75,7 @@ struct SimParams {
   int no_mirror;         // coefficient pass: write only the stored (upper) own-block tiles (dz_sym_kernel
                          // reads the lower ones transposed)
   // Fused normalisation backward (see dot_slots / dz_store):
-  float* dotp;           // coefficient pass: partials of dot_i = sum_j C_ij cos_ij, [Rpad][4 col_tiles]
+  float* dotp;           // coefficient pass: partials of dot_i = sum_j C_ij cos_ij, [4 col_tiles][Rpad]
   const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
   int nh_dt, nd;
   const float* ninv;     // ... 1 / |h_i|
@@ -167,8 +167,8 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
     mirror = reinterpret_cast<T*>(p.mbuf) + ((long long)(slot * rt + nt % rt) * rt + mt) * kTileElems;
   }
   // dot partial slots of row i: 4 per column tile J (the quarter of J's columns a wave covered, or
-  // for the column partials of a mirrored tile the quarter of its rows); each written once
-  const int nslot = 4 * p.col_tiles;
+  // for the column partials of a mirrored tile the quarter of its rows); each written once,
+  // slot-major ([slot][Rpad]: a store instruction's lanes hold neighbouring rows)
   const int wq = NW == 8 ? ((threadIdx.x >> 6) & 3) : (col_base >> 6);  // column quarter of this wave
   float cdot[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -205,7 +205,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         for (int ni = 0; ni < 4; ++ni) d += to_f32<T>(from_f32<T>(c[ni][r])) * acc[mi][ni][r];
         d = row16_sum(d);
         const int row = mt * kTile + rb[mi] + 4 * (lane >> 4) + r;
-        if ((lane & 15) == 0) p.dotp[(long long)row * nslot + nt * 4 + wq] = d;
+        if ((lane & 15) == 0) p.dotp[(long long)(nt * 4 + wq) * p.Rpad + row] = d;
       }
       const int h2 = NMI == 8 ? (mi >> 2) : 0;
 #pragma unroll
@@ -241,7 +241,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
           const float d = xrow_sum(cdot[h2][ni]);
           const int rq = NMI == 8 ? 2 * h2 + wa8 : (row_base >> 6);  // row quarter of this wave's rows
           const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
-          if (lane < 16) p.dotp[(long long)row * nslot + (p.row_tile0 + mt) * 4 + rq] = d;
+          if (lane < 16) p.dotp[(long long)((p.row_tile0 + mt) * 4 + rq) * p.Rpad + row] = d;
         }
     }
   }
@@ -344,7 +344,6 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
     scol[ni] = exp2i(e);
     icol[ni] = exp2i(-e);
   }
-  const int nslot = 4 * p.col_tiles;
   const int wq = col_base >> 6;
   float cdot[4] = {0.f, 0.f, 0.f, 0.f};
   const int qd = lane & 3;  // the row of a 4-row group this lane stores after the quad swap
@@ -411,7 +410,7 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float d = row16_sum(rdot[r]);
-        if ((lane & 15) == 0) p.dotp[(long long)(gi0 + r) * nslot + nt * 4 + wq] = d;
+        if ((lane & 15) == 0) p.dotp[(long long)(nt * 4 + wq) * p.Rpad + gi0 + r] = d;
       }
     }
   }
@@ -420,7 +419,7 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
     for (int ni = 0; ni < 4; ++ni) {
       const float d = xrow_sum(cdot[ni]);
       const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
-      if (lane < 16) p.dotp[(long long)row * nslot + (p.row_tile0 + mt) * 4 + (row_base >> 6)] = d;
+      if (lane < 16) p.dotp[(long long)((p.row_tile0 + mt) * 4 + (row_base >> 6)) * p.Rpad + row] = d;
     }
   }
   __syncthreads();
@@ -597,6 +596,14 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
     // the 16-byte chunk index XORed by (row & 15) (conflict-free both ways), then 512-byte
     // coalesced rows out. A fragment's direct 8-byte stores put 16 rows in every instruction.
     typedef __attribute__((address_space(3))) u32x2 lds_u2;
+    // fused normalisation backward: this thread's row statistics are loaded before the staging
+    // and its 16 chunks of h (16-bit inputs) right after it, so their latency hides under the
+    // staging and the barriers instead of following the tile's last MFMA one load at a time
+    float iv0 = 0.f, dt0 = 0.f;
+    if (p.ndh && tid < kTile && mt * kTile + tid < p.R) {
+      iv0 = p.ninv[mt * kTile + tid];
+      dt0 = p.ndot[mt * kTile + tid];
+    }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
       const int rt = rb[mi] + (lane & 15);
@@ -609,6 +616,18 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
         *(lds_u2*)(lds + rt * 512 + ((((ct >> 3) ^ (rt & 15))) << 4) + ((ct >> 2) & 1) * 8) = pk.u;
       }
     }
+    const bool h16 = p.ndh && p.nh_dt != 0;
+    u32x4 hq[16];
+    if (h16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
+        const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
+        hq[k] = (m < p.R && d0 < p.nd)
+                    ? *reinterpret_cast<const u32x4*>(static_cast<const char*>(p.nh) + ((long long)m * p.nd + d0) * 2)
+                    : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
     __syncthreads();
     if (p.ndh) {
       // Fused normalisation backward (replaces the norm_bwd launch and the dZ slab round trip):
@@ -619,14 +638,11 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
       typedef __attribute__((address_space(3))) float lds_fl;
       lds_fl* cf = (lds_fl*)(lds + kTile * 512);  // [256][2] per-row c1, c2
       if (tid < kTile) {
-        const int m = mt * kTile + tid;
-        const float iv = m < p.R ? p.ninv[m] : 0.f;
-        const float dt = m < p.R ? p.ndot[m] : 0.f;
-        cf[2 * tid] = sgo * iv;
-        cf[2 * tid + 1] = sgo * iv * iv * dt;
+        cf[2 * tid] = sgo * iv0;
+        cf[2 * tid + 1] = sgo * iv0 * iv0 * dt0;
       }
       __syncthreads();
-#pragma unroll 2
+#pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
         const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
@@ -638,12 +654,12 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
         float hv[8], o[8];
         if (p.nh_dt == 2) {
           union { __bf16 h[8]; u32x4 u; } x;
-          x.u = *reinterpret_cast<const u32x4*>(static_cast<const __bf16*>(p.nh) + off);
+          x.u = hq[k];
 #pragma unroll
           for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
         } else if (p.nh_dt == 1) {
           union { _Float16 h[8]; u32x4 u; } x;
-          x.u = *reinterpret_cast<const u32x4*>(static_cast<const _Float16*>(p.nh) + off);
+          x.u = hq[k];
 #pragma unroll
           for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
         } else {

@@ -50,6 +50,11 @@ class TrainConfig:
     warmup_steps: int = 10
     optimizer: str = "lars"          # lars | sgd | adamw
     amp: bool = True                 # bf16 autocast on the GPU
+    # GPU: run the step on a new high-priority stream ("high"), a new stream ("new") or the
+    # default stream ("default"). On the default stream RCCL kernels (DDP's bucket all-reduces,
+    # the NT-Xent transfers) shared its hardware queue and ran only between compute kernels
+    # (profiles/r3/overlap).
+    compute_stream: str = "high"
     compute: str = "auto"            # loss compute dtype
     negatives: str = "symmetric"     # multi-GPU negatives: symmetric | allgather | ring
     sync_bn: bool = True             # global BN statistics (SimCLR)
@@ -115,6 +120,8 @@ class SimCLRTrainer:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
+        if device.type == "cuda" and cfg.compute_stream != "default":
+            torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=-1 if cfg.compute_stream == "high" else 0))
         torch.manual_seed(cfg.seed)
         model = build_model(cfg).to(device)
         if device.type == "cuda":
