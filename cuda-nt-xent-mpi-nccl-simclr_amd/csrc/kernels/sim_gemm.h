@@ -33,6 +33,12 @@ namespace dev {
 enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
 
 constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 64 KiB
+// cache-policy bits of the GEMM operand LDS-DMA (0: default policy; experiment builds set
+// NTXENT_GEMM_DMA_AUX, e.g. 2 = nt, 1 = sc0: tools/build_variant.sh)
+#ifndef NTXENT_GEMM_DMA_AUX
+#define NTXENT_GEMM_DMA_AUX 0
+#endif
+constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
 constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
@@ -762,7 +768,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
-                                       (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, 0);
+                                       (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, kGemmDmaAux);
     s.advance(isB ? p.B : p.A);
   };
 

@@ -115,3 +115,30 @@ def test_dist_loss_on_rccl_world1(nccl_group, negatives):
     assert abs(l1.item() - l0.item()) <= 1e-5 * abs(l0.item())
     scale = g0.float().abs().max().item()
     assert (g1.float() - g0.float()).abs().max().item() <= 2e-2 * scale
+
+
+def test_dist_loss_on_compute_stream(nccl_group):
+    """The data-parallel step on a high-priority compute stream (use_compute_stream, as bench.py
+    and the trainer run it): same loss / gradient as on the default stream, and the transfer's
+    work handles order the compute stream correctly."""
+    import ntxent_amd
+    from ntxent_amd.parallel import use_compute_stream
+    from ntxent_amd.parallel.symmetric import SymNTXentFunction
+
+    _, h = _inputs(4096, 512, torch.bfloat16, seed=23)
+    x0 = h.clone().requires_grad_(True)
+    l0 = SymNTXentFunction.apply(x0, 0.1, "fp16", nccl_group)
+    (g0,) = torch.autograd.grad(l0, x0)
+    torch.cuda.synchronize()
+    old = torch.cuda.current_stream()
+    s = use_compute_stream()
+    try:
+        assert torch.cuda.current_stream() == s and s != torch.cuda.default_stream()
+        x1 = h.clone().requires_grad_(True)
+        l1 = SymNTXentFunction.apply(x1, 0.1, "fp16", nccl_group)
+        (g1,) = torch.autograd.grad(l1, x1)
+        torch.cuda.synchronize()
+    finally:
+        torch.cuda.set_stream(old)
+    assert l1.item() == l0.item()
+    assert torch.equal(g1, g0)
