@@ -357,10 +357,10 @@ int main(int argc, char** argv) {
     else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
     else if (a == "--no-dzsym") ntxent::set_dz_sym(false);
     else if (a == "--dzsym") ntxent::set_dz_sym(true);
-    else if (a == "--prefetch") ntxent::set_fwd_prefetch(true);
+    else if (a == "--fwd-stream") ntxent::set_fwd_stream(true);
     else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
-    else if (a == "--no-prefetch") ntxent::set_fwd_prefetch(false);
+    else if (a == "--no-fwd-stream") ntxent::set_fwd_stream(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "--negatives") {
@@ -383,7 +383,8 @@ int main(int argc, char** argv) {
                   "  --no-strips: forward remainder tiles by the stream-K split instead of diagonal strips (A/B)\n"
                   "  --dzsym / --no-dzsym: backward from the upper-triangular C + Zq (launch_dz_sym), or through\n"
                   "              mirrored coefficient tiles + ZqT + launch_dz (default)\n"
-                  "  --prefetch: forward GEMM issues the next item's prologue under the epilogue (A/B)\n");
+                  "  --no-fwd-stream: forward GEMM drains after each item and issues the next item's prologue\n"
+                  "              after its epilogue (A/B; default: the operand streams run into the next item)\n");
       return 0;
     }
   }

@@ -243,9 +243,10 @@ int lse_scratch_floats(const Geometry& g);
 // negatives-only max logit, log2 units), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
 // bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
 void set_fp8_backward(bool on);  // default: see ntxent_kernels.hip
-// Forward GEMM: issue the next work item's prologue DMA before the epilogue (default on; A/B)
-void set_fwd_prefetch(bool on);
-bool fwd_prefetch_enabled();
+// Forward GEMM: the operand streams run from one whole-tile work item into the next, so the next
+// item's first K-steps load under the epilogue (default on; off for A/B)
+void set_fwd_stream(bool on);
+bool fwd_stream_enabled();
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad

@@ -100,9 +100,11 @@ __device__ __forceinline__ int fp8_row_exp(float amax) {
 }
 
 // ---- wave64 cross-lane reductions ----------------------------------------------------
-// DPP row_ror within a 16-lane row: 0x120 + n.
+// DPP row_ror within a 16-lane row: 0x120 + n. bound_ctrl set (no lane of a rotation is out of
+// bounds, so results are unchanged): lets hipcc fold the move into the consuming add / max
+// (v_add_f32_dpp: one instruction per reduction step instead of a v_mov_b32_dpp + v_add pair).
 template <int CTRL> __device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
 }
 // Reduce across the 16 lanes of a DPP row (lanes sharing l>>4): every lane gets the result.
 __device__ __forceinline__ float row16_max(float x) {
@@ -133,6 +135,48 @@ __device__ __forceinline__ float xrow_sum(float x) {
 __device__ __forceinline__ float wave_sum(float x) {
   x = row16_sum(x);
   return xrow_sum(x);
+}
+
+// Untracked LDS accesses (inline asm; byte address in LDS). hipcc waits vmcnt(0) for every
+// in-flight LDS-DMA before a compiler-visible LDS access, whatever its address; a kernel that
+// keeps DMA in flight across an epilogue uses these for regions the DMA never writes, and waits
+// lgkmcnt itself (the reads below return only after their own wait).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lds_put_f2(unsigned addr, f32x2 v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+// four 8-byte reads at addr + {0, 1, 2, 3} * 2048
+__device__ __forceinline__ void lds_get4_f2(unsigned addr, f32x2& a, f32x2& b, f32x2& c, f32x2& d) {
+  asm volatile(
+      "ds_read_b64 %0, %4\n\t"
+      "ds_read_b64 %1, %4 offset:2048\n\t"
+      "ds_read_b64 %2, %4 offset:4096\n\t"
+      "ds_read_b64 %3, %4 offset:6144\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+      : "v"(addr)
+      : "memory");
+}
+// two 8-byte reads at addr + {0, 2048}
+__device__ __forceinline__ void lds_get2_f2(unsigned addr, f32x2& a, f32x2& b) {
+  asm volatile(
+      "ds_read_b64 %0, %2\n\t"
+      "ds_read_b64 %1, %2 offset:2048\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(a), "=&v"(b)
+      : "v"(addr)
+      : "memory");
+}
+
+// Wave-uniform 16-byte load of a read-only table (written before the launch) through the scalar
+// cache: counted by lgkmcnt, not vmcnt, so it neither waits for nor drains in-flight LDS-DMA
+// (hipcc loads such a descriptor with a vector load and waits vmcnt(0) at its first use).
+__device__ __forceinline__ int4 sload_int4(const int4* base, int idx) {
+  typedef int i4s __attribute__((ext_vector_type(4)));
+  i4s r;
+  const int4* a = base + __builtin_amdgcn_readfirstlane(idx);
+  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r) : "s"(a) : "memory");
+  return make_int4(r[0], r[1], r[2], r[3]);
 }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }

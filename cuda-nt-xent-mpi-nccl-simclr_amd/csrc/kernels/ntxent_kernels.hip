@@ -729,7 +729,6 @@ void dispatch_gemm(DType t, F&& f) {
 // the row's dim_k8 bytes), so accumulators are unscaled dot products like the other dtypes.
 void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
   p.acc_scale = p.y_scale;
-  p.cos_scale = 1.0f;
   p.scale_off = comp == DType::FP8 ? g.dim_k8 : 0;
 }
 
@@ -744,7 +743,7 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
 
 dev::SimParams base_params(const Geometry& g) {
   dev::SimParams p{};
-  p.fwd_prefetch = fwd_prefetch_enabled() ? 1 : 0;
+  p.fwd_stream = fwd_stream_enabled() ? 1 : 0;
   p.R = g.rows;
   p.Rpad = g.rows_pad;
   p.n_half = g.rows / 2;
@@ -756,7 +755,6 @@ dev::SimParams base_params(const Geometry& g) {
   p.c_tile0 = 0;
   p.y_scale = g.inv_temp * dev::kLog2e;
   p.acc_scale = p.y_scale;
-  p.cos_scale = 1.0f;
   p.fixed_shift = (2.0f * p.y_scale < 120.0f) ? 1 : 0;  // tau > ~0.024
   return p;
 }
@@ -1065,8 +1063,7 @@ static std::atomic<bool> g_dz_sym{false};        // dZ from the upper-triangular
                                                  // (profiles/r3/ab: its GEMM is slower than coef mirrors + ZqT save)
 static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
-static std::atomic<bool> g_fwd_prefetch{false};  // forward GEMM: next item's prologue under the epilogue (A/B:
-                                                 // no gain measured, profiles/r3/ab)
+static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1084,8 +1081,8 @@ int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
 int grid_reserve() { return g_grid_reserve.load(); }
 void set_dz_sym(bool on) { g_dz_sym = on; }
 bool dz_sym_enabled() { return g_dz_sym.load(); }
-void set_fwd_prefetch(bool on) { g_fwd_prefetch = on; }
-bool fwd_prefetch_enabled() { return g_fwd_prefetch.load(); }
+void set_fwd_stream(bool on) { g_fwd_stream = on; }
+bool fwd_stream_enabled() { return g_fwd_stream.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }

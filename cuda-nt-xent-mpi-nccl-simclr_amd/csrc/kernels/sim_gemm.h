@@ -13,7 +13,9 @@
 // half-tile is re-staged as soon as its last LDS read is one barrier behind, so loads run
 // ~1.75 K-steps ahead; every wait is a counted `s_waitcnt vmcnt(10)` (5 half-tiles still in
 // flight) followed by a raw s_barrier — no vmcnt(0) drains in the loop
-// (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4).
+// (cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4). The forward streams its
+// operands across whole-tile work items: the last two K-steps' prefetches load the next item's
+// first two, under the epilogue (see kStreamMode in the kernel).
 //
 // Accumulator acc[mi][ni] (mi < 8, ni < 4) covers tile rows rbase(mi)..+15 and columns
 // cbase(ni)..+15 with rbase(mi) = 128(mi>>2) + 64 wa + 16(mi&3), cbase(ni) = 128(ni>>1) +
@@ -62,7 +64,6 @@ struct SimParams {
   int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
   float acc_scale;       // logit (log2 units) per accumulator unit (y_scale)
-  float cos_scale;       // cosine per accumulator unit (1)
   int scale_off;         // fp8 operands: byte offset of each row's E8M0 scale (= K bytes of a row)
   int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
@@ -77,7 +78,7 @@ struct SimParams {
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
-  int fwd_prefetch;      // forward: issue the next item's prologue DMA before the epilogue
+  int fwd_stream;        // forward: operand streams run into the next whole-tile item (sim_gemm_kernel)
   int no_mirror;         // coefficient pass: write only the stored (upper) own-block tiles (dz_sym_kernel
                          // reads the lower ones transposed)
   // Fused normalisation backward (see dot_slots / dz_store):
@@ -112,21 +113,23 @@ struct SimParams {
 // fragment per 16-byte unit: (((rb >> 4) * 16 + (cb >> 4)) * 64 + lane) * 4.
 __device__ __forceinline__ int sc_unit(int rb, int cb, int lane) { return ((rb >> 4) * 8 + (cb >> 5)) * 64 + lane; }
 
-// One monotonically advancing K position of a staged half-tile stream (clamped at the last
-// K-step, so the trailing prefetches of the schedule re-read valid memory).
+// One monotonically advancing K position of a staged half-tile stream of one operand row tile
+// (clamped at the last K-step, so the trailing prefetches of the schedule re-read valid
+// memory; forward streaming re-initialises a stream onto the next item instead).
 struct KStream {
-  long long kin, kbo;
-  int left;
-  __device__ __forceinline__ void init(long long k0, const OperandDesc& o, int nk) {
-    kin = k0 % o.kblk;
-    kbo = (k0 / o.kblk) * o.kblk_stride;
+  const char* ptr;  // the K-step to stage next
+  int kin, left;    // byte offset inside its K block; K-steps after it
+  __device__ __forceinline__ void init(const char* base, long long k0, const OperandDesc& o, int nk) {
+    kin = (int)(k0 % o.kblk);
+    ptr = base + (k0 / o.kblk) * o.kblk_stride + kin;
     left = nk - 1;
   }
   __device__ __forceinline__ void advance(const OperandDesc& o) {
     if (left > 0) {
       --left;
+      ptr += kKStepBytes;
       kin += kKStepBytes;
-      if (kin == o.kblk) { kin = 0; kbo += o.kblk_stride; }
+      if (kin == o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }
     }
   }
 };
@@ -746,8 +749,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const int G = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, G);  // persistent block id (XCD-contiguous runs)
   const int nk = p.nk;                       // K-steps of a whole tile
-  const char* Ab = nullptr;
-  const char* Bb = nullptr;
   KStream sa0, sa1, sb0, sb1;
 
   // per-lane source offsets of this wave's two 8-row pieces of each half-tile
@@ -764,7 +765,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
-    const char* src = (isB ? Bb : Ab) + s.kbo + s.kin;
+    const char* src = s.ptr;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
@@ -871,6 +872,17 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   auto lds_drain = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
   // phase 1 issues the 8 A0 reads before the 4 B0 reads; LDS reads retire in order
   auto a0_retire = [&]() { asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); };
+  // Forward streaming (MODE == kModeFwd, 16-bit operands, whole-tile items): the operand
+  // streams run from one item into the next, so the schedule's trailing stages (K-steps n and
+  // n + 1 of an n-step item: A0 B0 B1 A1, A0 B0 B1 — exactly a prologue) stage the NEXT item's
+  // first two K-steps, and its epilogue runs with them in flight: no drain after the main loop,
+  // no prologue latency, only raw barriers and untracked (asm) LDS accesses in the epilogue (a
+  // __syncthreads or a compiler-tracked LDS access would wait vmcnt(0) for the in-flight DMA).
+  // The epilogue's kept-cosine stores are younger than those DMAs: they only make the next
+  // item's first counted waits stricter (vmcnt: all but the N youngest), so they drain under
+  // the exponentials and the first phases. (Waits relaxed by the store count for those phases
+  // measured slower: the per-phase selection cost more than the stores' drain.)
+  constexpr bool kStreamMode = MODE == kModeFwd && !kF8;
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
   auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
@@ -924,13 +936,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // operand streams of an item + its prologue DMA: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1
   // (the stream clamps keep the trailing prefetches in bounds, so every wait count is uniform)
   auto prologue = [&](int tile, int kb, int ke) {
-    const int4 tt = p.tiles[tile];
+    const int4 tt = sload_int4(p.tiles, tile);
     const int ns = ke - kb;
-    Ab = p.A.base + (long long)tt.x * p.A.row_tile_stride;
-    Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
+    const char* Ab = p.A.base + (long long)tt.x * p.A.row_tile_stride;
+    const char* Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
     const long long k0 = (long long)kb * kKStepBytes;
-    sa0.init(k0, p.A, ns); sa1.init(k0, p.A, ns);
-    sb0.init(k0, p.B, ns); sb1.init(k0, p.B, ns);
+    sa0.init(Ab, k0, p.A, ns); sa1.init(Ab, k0, p.A, ns);
+    sb0.init(Bb, k0, p.B, ns); sb1.init(Bb, k0, p.B, ns);
     if constexpr (kF8 && MODE != kModeDz) {
       // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
       // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a
@@ -942,22 +954,28 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
     stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
   };
-  // Forward: the next item's prologue is issued right after this item's stream-K fixup, so its
-  // DMA runs under the epilogue (exponentials, partial sums, cosine stores); the epilogue's LDS
-  // (row / column reductions) lives above the stage buffers for that. Younger epilogue stores
-  // only make the next item's counted waits stricter (vmcnt: all but the N youngest).
-  bool pre = false;
-  int ptile = 0, pkb = 0, pke = 0, pstile = -1;
+  // Forward streaming needs whole-tile items with an even number of >= 2 K-steps (the streams
+  // run two K-steps into the next item; even: its K-step 0 lands in buffer 0, as after a
+  // prologue).
+  const bool streaming = kStreamMode && p.fwd_stream && p.sk_tiles == 0 && nk >= 2 && (nk & 1) == 0;
+  bool streamed = false;  // this item's first two K-steps were staged by the previous item
   for (int item = 0;; ++item) {
   int tile, kb, ke, stile;
-  if (pre) {
-    tile = ptile; kb = pkb; ke = pke; stile = pstile;
-    pre = false;
+  if (streamed) {
+    tile = bid + item * G; kb = 0; ke = nk; stile = -1;
   } else {
     if (!fetch(item, tile, kb, ke, stile)) break;
     prologue(tile, kb, ke);
   }
-  const int4 t = p.tiles[tile];
+  const bool cont = streaming && item + 1 < n_dp;  // the trailing stages stage the next item
+  const char* na = nullptr;
+  const char* nb = nullptr;
+  if (cont) {
+    const int4 tn = sload_int4(p.tiles, bid + (item + 1) * G);
+    na = p.A.base + (long long)tn.x * p.A.row_tile_stride;
+    nb = p.B.base + (long long)(tn.y - p.b_tile0) * p.B.row_tile_stride;
+  }
+  const int4 t = sload_int4(p.tiles, tile);
   const int mt = t.x, nt = t.y;
   const int nsteps = ke - kb;
 #pragma unroll
@@ -970,6 +988,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if (grp == 1) barrier();  // stagger group 1 by one barrier
   for (int ks = 0; ks < nsteps; ++ks) {
     const int cur = ks & 1, nxt = cur ^ 1;
+    if constexpr (kStreamMode) {
+      // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
+      if (cont && ks == nsteps - 2) {
+        sa0.init(na, 0, p.A, nk); sb0.init(nb, 0, p.B, nk); sb1.init(nb, 0, p.B, nk);
+      }
+      if (cont && ks == nsteps - 1) sa1.init(na, 0, p.A, nk);
+    }
     dma_wait(); barrier();          // phase 1 L (wait covers B1(t) for phase 2)
     read_a(cur, 0, af);             //   operand reads first: their latency hides under the
     __builtin_amdgcn_sched_barrier(0);  // pin: the 8 A0 reads precede the B0 reads (a0_retire)
@@ -994,7 +1019,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     mma_quadrant(kI1, kI1, af, bf1);
   }
   if (grp == 0) barrier();  // re-align the groups
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
+  if (kStreamMode && cont) {
+    // the trailing stages are the next item's K-steps 0 and 1 (buffers of parity nk): leave
+    // them in flight; this epilogue's stores will be younger than them
+    streamed = true;
+  } else {
+    streamed = false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
+  }
   if constexpr (kF8 && MODE != kModeDz) {
     // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact, before any stream-K sum (acc row = rb +
     // 4 (lane >> 4) + r: four consecutive scale dwords; column = cb + (lane & 15))
@@ -1016,7 +1048,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   }
 
-  __syncthreads();
+  if constexpr (kStreamMode) {
+    lds_drain();  // raw barrier: a __syncthreads would drain the next item's DMA
+    barrier();
+  } else {
+    __syncthreads();
+  }
   {
   // Thread indices re-derived through an opaque copy: keeps the compiler from hoisting the
   // epilogue's address arithmetic out of the persistent loop, where it would stay live across
@@ -1032,12 +1069,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   for (int ni = 0; ni < 4; ++ni) cb[ni] = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
 
   if (nsteps != nk && !sk_fixup<kF8>(acc, p, stile, bid, G, tid, smem)) continue;
-  if constexpr (MODE == kModeFwd) {
-    if (p.fwd_prefetch && fetch(item + 1, ptile, pkb, pke, pstile)) {
-      prologue(ptile, pkb, pke);
-      pre = true;
-    }
-  }
 
   if constexpr (MODE == kModeDz) {
     if constexpr (kF8) dz8_finish(acc, p, mt, nt, rb, cb, lane);
@@ -1046,33 +1077,31 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
     const int kind = t.z;
-    if (p.sc) {  // keep cosines (compact slot per tile, canonical order)
-      typedef typename StoreT<T>::type TS;
-      TS* st = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-      const float cs = p.cos_scale;
+    // keep cosines (compact slot per tile, canonical order): the stores of 16-row block mi
+    typedef typename StoreT<T>::type TS;
+    TS* const st = p.sc ? reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems : nullptr;
+    auto store_cos = [&](int mi) {
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
+      for (int np = 0; np < 2; ++np) {
+        if constexpr (sizeof(TS) == 2) {
+          // 16-B stores (half the store-issue time of 8-B ones): the fragments of the column
+          // blocks cb and cb + 16 share one unit, see sc_unit()
+          union { TS h[8]; u32x4 u; } pk;
 #pragma unroll
-        for (int np = 0; np < 2; ++np) {
-          if constexpr (sizeof(TS) == 2) {
-            // 16-B stores (half the store-issue time of 8-B ones): the fragments of the column
-            // blocks cb and cb + 16 share one unit, see sc_unit()
-            union { TS h[8]; u32x4 u; } pk;
+          for (int r = 0; r < 4; ++r) {
+            pk.h[r] = from_f32<TS>(acc[mi][2 * np][r]);
+            pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r]);
+          }
+          *reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8) = pk.u;
+        } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              pk.h[r] = from_f32<TS>(acc[mi][2 * np][r] * cs);
-              pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r] * cs);
-            }
-            *reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8) = pk.u;
-          } else {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-              const int ni = 2 * np + q;
-              *reinterpret_cast<f32x4*>(st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4) = acc[mi][ni];
-            }
+          for (int q = 0; q < 2; ++q) {
+            const int ni = 2 * np + q;
+            *reinterpret_cast<f32x4*>(st + (((rb[mi] >> 4) * 16 + (cb[ni] >> 4)) * 64 + lane) * 4) = acc[mi][ni];
           }
         }
-    }
+      }
+    };
     // masks -> scaled logits in log2 units. The partials cover the NEGATIVES only: self and
     // positive are excluded (the positive logit comes from prep), so the loss is
     // softplus(lse_neg - y_pos) with no lse - y cancellation.
@@ -1085,52 +1114,61 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const bool col_out = kind == kTileSymOff || kind == kTileCross;  // column partials too
     constexpr bool fixed = FX != 0;  // launch_sim_gemm picks FX = p.fixed_shift
     const float M = p.y_scale;
-    // Masks, as a pre-pass that sets the masked raw values to -inf (exp2 -> 0). Element
-    // (tile row tr, tile col tc) is the self pair when tc - tr == r0 - c0 and a positive when
-    // tc - tr == r0 - c0 +- n_half; a 16x16 fragment can hold such an element only if its block
-    // offset cb - rb is within 15 of that difference, and padding only at the tile edge. These
-    // tests are wave-uniform, so only the few fragments that need it run per-lane selects; the
+    // Masks set the masked raw values of a 16-row block to -inf (exp2 -> 0). Element (tile row
+    // tr, tile col tc) is the self pair when tc - tr == r0 - c0 and a positive when tc - tr ==
+    // r0 - c0 +- n_half; a 16x16 fragment can hold such an element only if its block offset
+    // cb - rb is within 15 of that difference, and padding only at the tile edge. These tests
+    // are wave-uniform, so only the few fragments that need it run per-lane selects; the
     // per-element masked form compiled to per-element control flow (~15 us per tile) and the
     // fully unrolled select form spilled the main loop.
-    {
-      const int r0 = mt * kTile, c0 = col_local0;
-      const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
-      const bool pad = (r0 + kTile > p.R) || (c0 + kTile > p.R);
-      // fragment offsets cb - rb span [-240, 240]: only tiles with some |D| <= 255 hold a self
-      // or positive element (the diagonal band and the two positive bands of the own block)
-      const bool tile_near = own_blk && ((D0 <= 255 && D0 >= -255) || (D1 <= 255 && D1 >= -255) ||
-                                         (D2 <= 255 && D2 >= -255));
-      if (tile_near || pad) {
-        // block offsets from the wave index in an SGPR: the tests compile to scalar branches
-        const int ws = __builtin_amdgcn_readfirstlane(w);
-        const int was = ws >> 2, wbs = ws & 3;
+    const int r0 = mt * kTile, c0 = col_local0;
+    const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+    const bool pad = (r0 + kTile > p.R) || (c0 + kTile > p.R);
+    // fragment offsets cb - rb span [-240, 240]: only tiles with some |D| <= 255 hold a self
+    // or positive element (the diagonal band and the two positive bands of the own block)
+    const bool tile_near = own_blk && ((D0 <= 255 && D0 >= -255) || (D1 <= 255 && D1 >= -255) ||
+                                       (D2 <= 255 && D2 >= -255));
+    const bool mask_any = tile_near || pad;
+    // block offsets from the wave index in an SGPR: the tests compile to scalar branches
+    const int ws = __builtin_amdgcn_readfirstlane(w);
+    const int was = ws >> 2, wbs = ws & 3;
+    auto mask_rows = [&](int mi) {
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi)
+      for (int ni = 0; ni < 4; ++ni) {
+        const int rbs = 128 * (mi >> 2) + 64 * was + 16 * (mi & 3);
+        const int cbs = 128 * (ni >> 1) + 32 * wbs + 16 * (ni & 1);
+        const int off = cbs - rbs;
+        const bool near = tile_near && ((off - D0 <= 15 && D0 - off <= 15) || (off - D1 <= 15 && D1 - off <= 15) ||
+                                        (off - D2 <= 15 && D2 - off <= 15));
+        const bool edge = (r0 + rbs + 16 > p.R) || (c0 + cbs + 16 > p.R);
+        if (near || edge) {
+          const int tc = cb[ni] + (lane & 15);
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const int rbs = 128 * (mi >> 2) + 64 * was + 16 * (mi & 3);
-            const int cbs = 128 * (ni >> 1) + 32 * wbs + 16 * (ni & 1);
-            const int off = cbs - rbs;
-            const bool near = tile_near && ((off - D0 <= 15 && D0 - off <= 15) || (off - D1 <= 15 && D1 - off <= 15) ||
-                                          (off - D2 <= 15 && D2 - off <= 15));
-            const bool edge = (r0 + rbs + 16 > p.R) || (c0 + cbs + 16 > p.R);
-            if (near || edge) {
-              const int tc = cb[ni] + (lane & 15);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int tr = rb[mi] + 4 * (lane >> 4) + r;
-                const int gi = r0 + tr, d = tc - tr;
-                const bool drop = (gi >= p.R) | (c0 + tc >= p.R) |
-                                  (tile_near & ((d == D0) | ((d == D1) & (gi < p.n_half)) | ((d == D2) & (gi >= p.n_half))));
-                acc[mi][ni][r] = drop ? kNegInf : acc[mi][ni][r];
-              }
-            }
+          for (int r = 0; r < 4; ++r) {
+            const int tr = rb[mi] + 4 * (lane >> 4) + r;
+            const int gi = r0 + tr, d = tc - tr;
+            const bool drop = (gi >= p.R) | (c0 + tc >= p.R) |
+                              (tile_near & ((d == D0) | ((d == D1) & (gi < p.n_half)) | ((d == D2) & (gi >= p.n_half))));
+            acc[mi][ni][r] = drop ? kNegInf : acc[mi][ni][r];
           }
+        }
+      }
+    };
+    if constexpr (!fixed) {
+      if (st) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) store_cos(mi);
+      }
+      if (mask_any) {
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) mask_rows(mi);
       }
     }
     const float sc_ = p.acc_scale;
-    float2* rowred = reinterpret_cast<float2*>(smem + kFwdRed);                // [4 wb][256]
-    float2* colred = reinterpret_cast<float2*>(smem + kFwdRed + 4 * 256 * 8);  // [2 wa][256]
+    // row / column partial scratch above the stage buffers, [4 wb][256] and [2 wa][256] float2,
+    // written and read by untracked LDS accesses (the next item's DMA may be in flight)
+    const unsigned rowred = (unsigned)(uintptr_t)(lds + kFwdRed);
+    const unsigned colred = rowred + 4 * 256 * 8;
     if constexpr (fixed) {
       // Streamed per 16-row block: exponentiate (exp2(-inf) = 0 for the masked elements),
       // reduce the 4 rows, fold into the column sums; acc[mi] is dead afterwards, which keeps
@@ -1138,6 +1176,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       float csum[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
+        // this block's cosine stores go out between the exponentials of the blocks: the CU's
+        // store stream (HBM-write-bound while every CU ends a tile) drains under the VALU work
+        // instead of stalling every wave at its 16th store before any exponential
+        if (st) store_cos(mi);
+        if (mask_any) mask_rows(mi);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -1147,7 +1190,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
           s = row16_sum(s);
           // every lane of the 16-lane row holds the sum: all write it (no exec-masked block)
-          rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(s > 0.f ? M : kNegInf, s);
+          lds_put_f2(rowred + 8 * (wb * 256 + rb[mi] + 4 * (lane >> 4) + r), f32x2{s > 0.f ? M : kNegInf, s});
         }
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
@@ -1158,7 +1201,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const float s = xrow_sum(csum[ni]);
-          colred[wa * 256 + cb[ni] + (lane & 15)] = make_float2(s > 0.f ? M : kNegInf, s);
+          lds_put_f2(colred + 8 * (wa * 256 + cb[ni] + (lane & 15)), f32x2{s > 0.f ? M : kNegInf, s});
         }
       }
     } else {
@@ -1178,7 +1221,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           float s = fast_exp2(acc[mi][0][r] - ms) + fast_exp2(acc[mi][1][r] - ms) +
                     fast_exp2(acc[mi][2][r] - ms) + fast_exp2(acc[mi][3][r] - ms);
           s = row16_sum(s);
-          rowred[wb * 256 + rb[mi] + 4 * (lane >> 4) + r] = make_float2(m, s);
+          lds_put_f2(rowred + 8 * (wb * 256 + rb[mi] + 4 * (lane >> 4) + r), f32x2{m, s});
         }
       if (col_out) {  // column partials = partials of the mirrored rows
 #pragma unroll
@@ -1196,25 +1239,28 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
             for (int r = 0; r < 4; ++r) s += fast_exp2(acc[mi][ni][r] - ms);
           s = xrow_sum(s);
-          colred[wa * 256 + cb[ni] + (lane & 15)] = make_float2(m, s);
+          lds_put_f2(colred + 8 * (wa * 256 + cb[ni] + (lane & 15)), f32x2{m, s});
         }
       }
     }
-    __syncthreads();
+    lds_drain();  // the untracked partial writes
+    if constexpr (kStreamMode) {
+      barrier();
+    } else {
+      __syncthreads();
+    }
     if (tid < 256) {
-      float2 v = rowred[tid];
-      float m = v.x, s = v.y;
+      f32x2 v[4];
+      lds_get4_f2(rowred + 8 * tid, v[0], v[1], v[2], v[3]);
+      float m = v[0].x, s = v[0].y;
 #pragma unroll
-      for (int q = 1; q < 4; ++q) {
-        const float2 u = rowred[q * 256 + tid];
-        lse_merge(m, s, u.x, u.y);
-      }
+      for (int q = 1; q < 4; ++q) lse_merge(m, s, v[q].x, v[q].y);
       p.part[(long long)nt * p.Rpad + mt * kTile + tid] = make_float2(m, s);
     } else if (col_out) {
       const int c = tid - 256;
-      float2 v = colred[c];
+      f32x2 v, u;
+      lds_get2_f2(colred + 8 * c, v, u);
       float m = v.x, s = v.y;
-      const float2 u = colred[256 + c];
       lse_merge(m, s, u.x, u.y);
       if (kind == kTileSymOff) {
         p.part[(long long)(p.row_tile0 + mt) * p.Rpad + (nt - p.row_tile0) * kTile + c] = make_float2(m, s);
@@ -1225,7 +1271,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   }
   }  // epilogue scope
-  __syncthreads();  // LDS of this item's epilogue is reused by the next item's staging
+  // LDS of this item's epilogue is reused by the next item's staging (streaming: the partial
+  // scratch lies above the stage buffers and the next epilogue writes it after the next main
+  // loop's barriers, so no barrier here)
+  if constexpr (!kStreamMode) __syncthreads();
   }  // work items
 }
 
@@ -1363,22 +1412,21 @@ __global__ __launch_bounds__(256) void diag_strip_kernel(const SimParams p) {
   const int rb0 = 16 * strip;
   if (p.sc) {  // kept cosines, canonical fragment order (sc_unit), before the masks
     TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-    const float cs = p.cos_scale;
     if constexpr (sizeof(TS) == 2) {
 #pragma unroll
       for (int np = 0; np < 2; ++np) {
         union { TS h[8]; u32x4 u; } pk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pk.h[r] = from_f32<TS>(acc[2 * np][r] * cs);
-          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r] * cs);
+          pk.h[r] = from_f32<TS>(acc[2 * np][r]);
+          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r]);
         }
         *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * w + 32 * np, lane) * 8) = pk.u;
       }
     } else {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
-        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * w + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f] * cs;
+        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * w + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f];
     }
   }
   const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
@@ -1514,22 +1562,21 @@ __global__ __launch_bounds__(256) void diag_sub_kernel(const SimParams p, float2
   const int rb0 = 64 * a + 16 * w;
   if (p.sc) {  // kept cosines, canonical fragment order, before the masks
     TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-    const float cs = p.cos_scale;
     if constexpr (sizeof(TS) == 2) {
 #pragma unroll
       for (int np = 0; np < 2; ++np) {
         union { TS h[8]; u32x4 u; } pk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pk.h[r] = from_f32<TS>(acc[2 * np][r] * cs);
-          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r] * cs);
+          pk.h[r] = from_f32<TS>(acc[2 * np][r]);
+          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r]);
         }
         *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * np, lane) * 8) = pk.u;
       }
     } else {
 #pragma unroll
       for (int f = 0; f < 4; ++f)
-        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * b + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f] * cs;
+        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * b + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f];
     }
   }
   const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
@@ -1645,22 +1692,21 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
   }
   if (p.sc) {  // kept cosines (canonical fragment order), before the masks
     TS* st = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-    const float cs = p.cos_scale;
     if constexpr (sizeof(TS) == 2) {
 #pragma unroll
       for (int np = 0; np < 2; ++np) {
         union { TS h[8]; u32x4 u; } pk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pk.h[r] = from_f32<TS>(v[2 * np][r] * cs);
-          pk.h[4 + r] = from_f32<TS>(v[2 * np + 1][r] * cs);
+          pk.h[r] = from_f32<TS>(v[2 * np][r]);
+          pk.h[4 + r] = from_f32<TS>(v[2 * np + 1][r]);
         }
         *reinterpret_cast<u32x4*>(st + sc_unit(s16, 64 * w + 32 * np, lane) * 8) = pk.u;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<f32x4*>(st + (((s16 >> 4) * 16 + ((64 * w + 16 * j) >> 4)) * 64 + lane) * 4) = v[j] * cs;
+        *reinterpret_cast<f32x4*>(st + (((s16 >> 4) * 16 + ((64 * w + 16 * j) >> 4)) * 64 + lane) * 4) = v[j];
     }
   }
   const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;

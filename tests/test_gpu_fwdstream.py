@@ -1,0 +1,67 @@
+"""Forward similarity GEMM with operand streaming across work items (sim_gemm_kernel, MODE
+kModeFwd: the trailing stages of one whole-tile item stage the next item's first two K-steps
+and its epilogue runs with them in flight) vs the drained schedule (set_fwd_stream(False)).
+
+Each tile's MFMA order is the same either way, so the LSE partials, the kept cosines, the loss
+and the gradient must agree bitwise; shapes with >= 2 whole-tile rounds per block (2N >= 8192
+rows: 528+ tiles on 256 CUs) exercise the hand-over, fp32 operands the 32-store epilogue.
+"""
+import pytest
+import torch
+
+from test_gpu_kernels import _inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_stream(C, on, fn):
+    old = C.fwd_stream_enabled()
+    C.set_fwd_stream(on)
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out
+    finally:
+        C.set_fwd_stream(old)
+
+
+@pytest.mark.parametrize("rows,dim,compute", [
+    (8192, 256, "fp16"),     # 2 whole-tile rounds per block
+    (12288, 512, "bf16"),    # 4 rounds + remainder
+    (8192, 128, "fp32"),     # f32 kept cosines: 32 epilogue stores per wave
+    (8192, 2048, "fp16"),    # headline shape
+])
+def test_fwd_stream_stats_bitwise(ext, rows, dim, compute):
+    C = ext
+    assert C.fwd_stream_enabled(), "streaming is the default"
+    _, h = _inputs(rows, dim, torch.float32 if compute == "fp32" else torch.bfloat16, seed=31)
+    plan = C.get_plan(rows, dim, 1, 0, 0.07, compute, 0)
+    assert not plan.small
+    zq, inv, ypos, _ = C.prep(h, plan)
+
+    def fwd():
+        part, sc = C.fwd_stats(zq, zq, plan, True)
+        return part.clone(), sc.clone()
+
+    a = _with_stream(C, True, fwd)
+    b = _with_stream(C, False, fwd)
+    assert torch.equal(a[1], b[1]), "kept cosines differ"
+    assert torch.equal(a[0], b[0]), "LSE partials differ"
+
+
+@pytest.mark.parametrize("rows,dim,compute", [(8192, 512, "fp16"), (16384, 256, "bf16")])
+def test_fwd_stream_loss_grad_bitwise(ext, rows, dim, compute):
+    import ntxent_amd
+
+    _, h = _inputs(rows, dim, torch.bfloat16, seed=37)
+
+    def step():
+        x = h.clone().requires_grad_(True)
+        loss = ntxent_amd.ntxent_loss(x, 0.07, compute=compute)
+        (g,) = torch.autograd.grad(loss, x)
+        return loss.detach(), g
+
+    la, ga = _with_stream(ext, True, step)
+    lb, gb = _with_stream(ext, False, step)
+    assert torch.equal(la, lb)
+    assert torch.equal(ga, gb)
