@@ -361,6 +361,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
     else if (a == "--no-fwd-stream") ntxent::set_fwd_stream(false);
+    else if (a == "--no-sk-pm") ntxent::set_splitk_piece_major(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "--negatives") {
@@ -384,7 +385,8 @@ int main(int argc, char** argv) {
                   "  --dzsym / --no-dzsym: backward from the upper-triangular C + Zq (launch_dz_sym), or through\n"
                   "              mirrored coefficient tiles + ZqT + launch_dz (default)\n"
                   "  --no-fwd-stream: forward GEMM drains after each item and issues the next item's prologue\n"
-                  "              after its epilogue (A/B; default: the operand streams run into the next item)\n");
+                  "              after its epilogue (A/B; default: the operand streams run into the next item)\n"
+                  "  --no-sk-pm: split-K forward with the tile-major straddling pieces (A/B; default piece-major)\n");
       return 0;
     }
   }

@@ -247,6 +247,10 @@ void set_fp8_backward(bool on);  // default: see ntxent_kernels.hip
 // item's first K-steps load under the epilogue (default on; off for A/B)
 void set_fwd_stream(bool on);
 bool fwd_stream_enabled();
+// Split-K forward (tile-starved shapes): tile-aligned K pieces assigned piece-major to the blocks
+// (default on; off: the flattened tile-major split with straddling pieces, for A/B)
+void set_splitk_piece_major(bool on);
+bool splitk_piece_major();
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad

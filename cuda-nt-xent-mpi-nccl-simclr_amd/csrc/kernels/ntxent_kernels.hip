@@ -1064,6 +1064,7 @@ static std::atomic<bool> g_dz_sym{false};        // dZ from the upper-triangular
 static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
 static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
+static std::atomic<bool> g_sk_piece_major{true};  // split-K forward: tile-aligned pieces, piece-major blocks
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1082,6 +1083,8 @@ int grid_reserve() { return g_grid_reserve.load(); }
 void set_dz_sym(bool on) { g_dz_sym = on; }
 bool dz_sym_enabled() { return g_dz_sym.load(); }
 void set_fwd_stream(bool on) { g_fwd_stream = on; }
+void set_splitk_piece_major(bool on) { g_sk_piece_major = on; }
+bool splitk_piece_major() { return g_sk_piece_major.load(); }
 bool fwd_stream_enabled() { return g_fwd_stream.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
@@ -1137,10 +1140,18 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
     p.dp_tiles = 0;
     p.sk_tiles = ntiles;
     p.ipb = (nk_tile + pieces - 1) / pieces;
-    p.sk_out = 1;
     p.sk_cnt = static_cast<int*>(ws.ptr);
     p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-    grid = (int)(((long long)ntiles * nk_tile + p.ipb - 1) / p.ipb);
+    if (splitk_piece_major()) {
+      // tile-aligned pieces, piece-major over the blocks: the XCD-contiguous block runs then
+      // stream one K range of every row panel together (L2 reuse across the tiles) instead of
+      // every K range of a few tiles (profiles/r3/splitk_pm)
+      p.sk_out = 2;
+      grid = (int)((nk_tile + p.ipb - 1) / p.ipb) * ntiles;
+    } else {
+      p.sk_out = 1;
+      grid = (int)(((long long)ntiles * nk_tile + p.ipb - 1) / p.ipb);
+    }
     NTXENT_CHECK(grid <= ws.num_cus && ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
                  "split-K forward: workspace too small");
   } else {

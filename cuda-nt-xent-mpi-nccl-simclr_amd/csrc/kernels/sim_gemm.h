@@ -104,6 +104,8 @@ struct SimParams {
   float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
   int* sk_cnt;           // [sk_tiles] arrival counters (zero at launch; self-cleaning)
   int sk_out;            // forward split-K: every piece only publishes its slab; sk_reduce_kernel
+                         // (2: tile-aligned pieces of ipb K-steps, piece-major: block b = piece
+                         // (b / sk_tiles) of tile (b % sk_tiles), slab slot 2 b + 1)
                          // sums a tile's slabs and runs its epilogue in row / column strips
 };
 
@@ -475,7 +477,7 @@ __device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[8][4], const SimParams& p,
   const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
   auto slot_off = [&](int bb) {  // byte offset of block bb's slab for this tile
     const long long s = (long long)bb * p.ipb;
-    const bool first_partial = (s / nk == stile) && (s % nk != 0);
+    const bool first_partial = p.sk_out != 2 && (s / nk == stile) && (s % nk != 0);
     return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
   };
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
@@ -923,6 +925,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       tile = bid + item * G;
       kb = 0;
       ke = nk;
+      return true;
+    }
+    if (p.sk_out == 2) {  // piece-major aligned split: one piece per block
+      if (item > 0) return false;
+      stile = bid % p.sk_tiles;
+      kb = (int)((bid / p.sk_tiles) * p.ipb);
+      ke = kb + (int)p.ipb < nk ? kb + (int)p.ipb : nk;
+      tile = p.dp_tiles + stile;
       return true;
     }
     if (it >= it1) return false;
@@ -1657,7 +1667,12 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
   const int s16 = 16 * strip;
   const int nk = p.nk;
   const long long ipb = p.ipb;
-  const int b0 = (int)((long long)tile * nk / ipb), b1 = (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  // the tile's pieces: contiguous blocks b0..b1 (tile-major split) or blocks pc * sk_tiles + tile,
+  // pc = 0 .. npc - 1 (piece-major aligned split, sk_out == 2); summed in piece order
+  const bool pm = p.sk_out == 2;
+  const int npc = pm ? (int)((nk + ipb - 1) / ipb) : 0;
+  const int b0 = pm ? 0 : (int)((long long)tile * nk / ipb);
+  const int b1 = pm ? npc - 1 : (int)(((long long)(tile + 1) * nk - 1) / ipb);
   // this thread's 4 fragments (s16, cb[j] = 64 w + 16 j), MFMA C layout: rows s16 + r4 + r,
   // column cb[j] + c1; a wave reads 1 KiB contiguous per fragment and slab
   const int r4 = 4 * (lane >> 4), c1 = lane & 15;
@@ -1668,7 +1683,8 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
-  auto slab = [&](int bb) {
+  auto slab = [&](int bb) {  // bb: block (tile-major) or piece (piece-major)
+    if (pm) return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems;
     const long long st = (long long)bb * ipb;
     const bool first_partial = (st / nk == tile) && (st % nk != 0);
     return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;

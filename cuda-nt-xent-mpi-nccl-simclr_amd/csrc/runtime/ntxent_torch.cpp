@@ -960,6 +960,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
   m.def("set_fwd_stream", &ntxent::set_fwd_stream, py::arg("on"));
   m.def("fwd_stream_enabled", &ntxent::fwd_stream_enabled);
+  m.def("set_splitk_piece_major", &ntxent::set_splitk_piece_major, py::arg("on"));
+  m.def("splitk_piece_major", &ntxent::splitk_piece_major);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
   m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);

@@ -65,3 +65,33 @@ def test_fwd_stream_loss_grad_bitwise(ext, rows, dim, compute):
     lb, gb = _with_stream(ext, False, step)
     assert torch.equal(la, lb)
     assert torch.equal(ga, gb)
+
+
+@pytest.mark.parametrize("rows,dim,compute", [(2048, 8192, "fp16"), (1024, 4096, "bf16"), (2048, 4096, "fp8")])
+def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
+    """Tile-starved forward (split-K + sk_reduce): the piece-major aligned split against the
+    tile-major straddling one (different K pieces, so equal to fp32 rounding) and the loss
+    against the fp64 oracle."""
+    import ntxent_amd
+    from test_gpu_kernels import _oracle
+
+    _, h = _inputs(rows, dim, torch.bfloat16, seed=41)
+    old = ext.splitk_piece_major()
+    outs = {}
+    try:
+        for pm in (True, False):
+            ext.set_splitk_piece_major(pm)
+            x = h.clone().requires_grad_(True)
+            loss = ntxent_amd.ntxent_loss(x, 0.07, compute=compute)
+            (g,) = torch.autograd.grad(loss, x)
+            torch.cuda.synchronize()
+            outs[pm] = (loss.item(), g.float())
+    finally:
+        ext.set_splitk_piece_major(old)
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    assert abs(la - lb) <= 1e-5 * abs(lb)
+    scale = gb.abs().max().item()
+    assert (ga - gb).abs().max().item() <= 1e-2 * scale
+    if compute != "fp8":
+        lo, _ = _oracle(h, 0.07)
+        assert abs(la - lo) <= 2e-4 * abs(lo)
