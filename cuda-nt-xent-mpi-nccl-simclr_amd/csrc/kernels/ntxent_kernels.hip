@@ -1365,10 +1365,15 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     p.dp_tiles = 0;
     p.sk_tiles = ntiles;
     p.ipb = (nk + pieces - 1) / pieces;
-    p.sk_out = 1;
     p.sk_cnt = static_cast<int*>(ws.ptr);
     p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-    grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
+    if (splitk_piece_major()) {  // as the forward's: an XCD streams one K range of every panel
+      p.sk_out = 2;
+      grid = (int)((nk + p.ipb - 1) / p.ipb) * ntiles;
+    } else {
+      p.sk_out = 1;
+      grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
+    }
     NTXENT_CHECK(p.kbytes % kKStepBytes == 0 && grid <= ws.num_cus && ws.ptr != nullptr &&
                      ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
                  "split-K dZ: workspace too small");

@@ -1809,9 +1809,14 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
   const int mt = t.x, nt = t.y;
   const int nk = p.nk;
   const long long ipb = p.ipb;
-  const int b0 = (int)((long long)tile * nk / ipb), b1 = (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  // the tile's pieces: tile-major contiguous blocks b0..b1, or piece-major (sk_out == 2, see
+  // sk_reduce_kernel): piece pc is block pc * sk_tiles + tile
+  const bool pm = p.sk_out == 2;
+  const int b0 = pm ? 0 : (int)((long long)tile * nk / ipb);
+  const int b1 = pm ? (int)((nk + ipb - 1) / ipb) - 1 : (int)(((long long)(tile + 1) * nk - 1) / ipb);
   const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
   auto slab = [&](int bb) {
+    if (pm) return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems;
     const long long st = (long long)bb * ipb;
     const bool first_partial = (st / nk == tile) && (st % nk != 0);
     return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;

@@ -67,9 +67,10 @@ def test_fwd_stream_loss_grad_bitwise(ext, rows, dim, compute):
     assert torch.equal(ga, gb)
 
 
-@pytest.mark.parametrize("rows,dim,compute", [(2048, 8192, "fp16"), (1024, 4096, "bf16"), (2048, 4096, "fp8")])
+@pytest.mark.parametrize("rows,dim,compute", [(2048, 8192, "fp16"), (1024, 4096, "bf16"), (2048, 4096, "fp8"),
+                                              (8192, 512, "fp16")])  # last: split-K dZ only
 def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
-    """Tile-starved forward (split-K + sk_reduce): the piece-major aligned split against the
+    """Tile-starved forward and dZ (split-K + reduce launch): the piece-major aligned split against the
     tile-major straddling one (different K pieces, so equal to fp32 rounding) and the loss
     against the fp64 oracle."""
     import ntxent_amd
