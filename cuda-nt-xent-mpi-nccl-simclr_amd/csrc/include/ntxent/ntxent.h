@@ -99,7 +99,10 @@ Geometry make_geometry(int rows, int dim, int world, int rank, float temperature
 // Tile kinds of the forward / coefficient pass. kTileCross: a tile of another rank's column
 // block that this rank computes for BOTH ranks (symmetric data-parallel mode): its column
 // partials and mirrored coefficients go to per-partner buffers instead of this rank's own.
-enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2, kTileCross = 3 };
+enum TileKind : int { kTilePlain = 0, kTileDiag = 1, kTileSymOff = 2, kTileCross = 3,
+                      // coefficient pass only: an upper off-diagonal 64x64 region of a diagonal tile,
+                      // written with its mirror (the transposed region of the same tile)
+                      kTileDiagUp = 4 };
 
 // Symmetric data-parallel mode: rank `rank` computes rows [m0, m1) (its row tiles) x columns
 // [k0, k1) (rank q's row tiles) of the similarity block (rank, q); each unordered rank pair's
@@ -251,6 +254,10 @@ bool fwd_stream_enabled();
 // (default on; off: the flattened tile-major split with straddling pieces, for A/B)
 void set_splitk_piece_major(bool on);
 bool splitk_piece_major();
+// Diagonal remainder of the forward: upper 64x64 regions only, K halves for the off-diagonal ones
+// (diag_up_kernel; default on; off: all 16 regions over the whole K, diag_sub_kernel)
+void set_diag_upper(bool on);
+bool diag_upper_enabled();
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad

@@ -1065,6 +1065,7 @@ static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in th
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
 static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
 static std::atomic<bool> g_sk_piece_major{true};  // split-K forward: tile-aligned pieces, piece-major blocks
+static std::atomic<bool> g_diag_up{true};        // diagonal remainder: upper regions only (diag_up_kernel)
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
 void set_diag_strips(bool on) { g_diag_strips = on; }
 bool diag_strips_enabled() { return g_diag_strips.load(); }
@@ -1084,6 +1085,8 @@ void set_dz_sym(bool on) { g_dz_sym = on; }
 bool dz_sym_enabled() { return g_dz_sym.load(); }
 void set_fwd_stream(bool on) { g_fwd_stream = on; }
 void set_splitk_piece_major(bool on) { g_sk_piece_major = on; }
+void set_diag_upper(bool on) { g_diag_up = on; }
+bool diag_upper_enabled() { return g_diag_up.load(); }
 bool splitk_piece_major() { return g_sk_piece_major.load(); }
 bool fwd_stream_enabled() { return g_fwd_stream.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
@@ -1180,12 +1183,25 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // blocks (config 2, d = 512: strips 7.4 vs sub-tiles 8.0 us; headline 17.0 vs 15.3,
         // config 5 18.5 vs 12.9: profiles/r2/subtiles)
         const bool sub = (p.kbytes / kKStepBytes) >= 16 || !one_wave;
+        const int nk_d = (int)(p.kbytes / kKStepBytes);
         if (g_diag_sub.load() && sub && 4 * nstrip <= 2 * ws.num_cus) {
           q.sk_cnt = static_cast<int*>(ws.ptr);
           float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                       (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
-          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
-          else hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
+          // upper regions only (the coefficient pass mirrors a diagonal tile's regions), K halves
+          // for the off-diagonal ones: 10 tickets per tile, pair partials in the (idle) slab area.
+          // Measured (profiles/r3/diag_up): 14.4 vs 15.1 us at the headline (16 tiles, one block
+          // per CU), 13.7 vs 13.1 us at config 5 (32 tiles, two per CU): used for one wave only
+          if (g_diag_up.load() && nk_d >= 4 && one_wave && 10 * nstrip <= 2 * ws.num_cus &&
+              (size_t)12 * nstrip * 4096 <= (size_t)2 * ws.num_cus * kTileElems) {
+            q.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
+          } else if (p.fixed_shift) {
+            hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
+          } else {
+            hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
+          }
         } else if (p.fixed_shift) {
           if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 3>), sg, dim3(256), 0, stream, q);
           else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q);

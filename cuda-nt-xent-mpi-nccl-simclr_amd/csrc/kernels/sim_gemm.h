@@ -170,7 +170,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
   T* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
   T* mirror = nullptr;
-  if (kind == kTileSymOff && !p.no_mirror)
+  if ((kind == kTileSymOff && !p.no_mirror) || kind == kTileDiagUp)  // (kTileDiagUp: the same tile's slot)
     mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
   else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
     const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
@@ -243,7 +243,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
     }
   }
   if (p.dotp) {
-    if (kind == kTileSymOff) {
+    if (kind == kTileSymOff || kind == kTileDiagUp) {
       const int wa8 = (threadIdx.x >> 6) >> 2;
 #pragma unroll
       for (int h2 = 0; h2 < (NMI == 8 ? 2 : 1); ++h2)
@@ -334,7 +334,7 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   lds_char* ld_m = lds + 64 * S8;   // mirror: [64 cols][64 rows]
   unsigned char* base = reinterpret_cast<unsigned char*>(p.cbuf);
   unsigned char* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
-  unsigned char* mirror = kind == kTileSymOff
+  unsigned char* mirror = (kind == kTileSymOff || kind == kTileDiagUp)
                               ? base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems
                               : nullptr;
   const int col_local0 = (nt * kTile) % p.Rpad;
@@ -425,7 +425,7 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
       }
     }
   }
-  if (p.dotp && kind == kTileSymOff) {
+  if (p.dotp && (kind == kTileSymOff || kind == kTileDiagUp)) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const float d = xrow_sum(cdot[ni]);
@@ -1300,6 +1300,15 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   const int tidx = idx >> 4, w = (idx >> 1) & 7, half = idx & 1;
   const int wm = w >> 2, wn = w & 3;
   const int4 t = p.tiles[tidx];
+  // A diagonal tile is symmetric: only its regions a <= b (64-row group a = 2 wm + half, column
+  // group b = wn) are read, a region a < b writes C with its mirror (b, a) in the same tile, and
+  // the kept cosines of its lower regions may be absent (diag_up_kernel computes only the upper).
+  int kind = t.z;
+  if (kind == kTileDiag) {
+    const int ga = 2 * wm + half;
+    if (ga > wn) return;
+    if (ga < wn) kind = kTileDiagUp;
+  }
   const T* st = reinterpret_cast<const T*>(p.sc) + (long long)tidx * kTileElems;
   int rb[4], cb[4];
   f32x4 acc[4][4];
@@ -1325,9 +1334,9 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
       }
     }
   if constexpr (Q8)
-    coef_epilogue_q8<T>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+    coef_epilogue_q8<T>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, kind, (lds_char*)smem, p, lane);
   else
-    coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, t.z, (lds_char*)smem, p, lane);
+    coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, kind, (lds_char*)smem, p, lane);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1634,6 +1643,236 @@ __global__ __launch_bounds__(256) void diag_sub_kernel(const SimParams p, float2
 #pragma unroll
   for (int k = 1; k < 4; ++k) lse_merge(m, s, __uint_as_float(q[k][0]), __uint_as_float(q[k][1]));
   p.part[(long long)nt * p.Rpad + r0 + 64 * a + i] = make_float2(m, s);
+}
+
+// ------------------------------------------------------------------------------------
+// Diagonal tiles by their upper 64x64 regions only (the coefficient pass mirrors a diagonal
+// tile's regions a < b into (b, a), coef_kernel), 16 blocks per tile that each stream the same
+// operand bytes (the remainder is bound by the per-CU load path, so balance is the lever):
+//   blocks 0-3: the diagonal regions (a, a) over the whole K, 64 rows staged (A = B);
+//   blocks 4-15: the six regions a < b, each as two K halves, 128 rows staged.
+// The second half of a region to arrive (ticket) adds the first one's fp32 partial (write-through
+// slab, as sk_fixup) and runs the epilogue: kept cosines of (a, b), masks, row partials of group
+// a over b's 64 columns and column partials of group b over a's 64 rows (the mirrored region's
+// row partials). The 4th contribution to a row group (ticket) merges the 4 in b order, so the
+// result does not depend on arrival order. Half the L2 -> CU bytes of diag_sub_kernel; the
+// loop is bound by load latency over the few K-steps in flight, so the diagonal-region blocks
+// (half the rows per K-step) run a 6-stage ring of 8 KiB stages in the same LDS (5 in flight).
+// ------------------------------------------------------------------------------------
+constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + column-partial exchange + flags
+template <typename T, int FX>
+__global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch) {
+  using MM = Mfma<T>;
+  typedef typename MM::frag frag;
+  typedef typename StoreT<T>::type TS;
+  typedef __attribute__((address_space(3))) const frag lds_frag;
+  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array (see diag_strip_body)
+  lds_char* lds = (lds_char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nt_d = gridDim.x >> 4;                    // diagonal tiles in this launch
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 blocks share one XCD
+  const int tile = idx >> 4, s = idx & 15;
+  const bool dg = s < 4;
+  const int q = dg ? 0 : (s - 4) >> 1, hk = dg ? 0 : (s - 4) & 1;
+  const int a = dg ? s : (q < 3 ? 0 : (q < 5 ? 1 : 2));
+  const int b = dg ? s : (q < 3 ? q + 1 : (q < 5 ? q - 1 : 3));
+  const int4 t = p.tiles[tile];
+  const int mt = t.x, nt = t.y;
+  const int nk = (int)(p.kbytes / kKStepBytes);
+  const int k0 = dg ? 0 : (hk == 0 ? 0 : nk / 2), k1 = dg ? nk : (hk == 0 ? nk / 2 : nk);
+  // DMA pieces: diagonal region 2 per wave (ring rows 16 w + 8 j + (lane >> 3) = A rows 64 a..),
+  // off-diagonal 4 per wave (ring rows 32 w + 8 j + ..: 0-63 A = rows 64 a.., 64-127 B = 64 b..)
+  const int np = dg ? 2 : 4;
+  const char* src[4];
+  int ldst[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = dg ? 16 * w + 8 * j + (lane >> 3) : 32 * w + 8 * j + (lane >> 3);
+    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
+    ldst[j] = (dg ? 16 * w + 8 * j : 32 * w + 8 * j) * kKStepBytes;
+    src[j] = row < 64 ? p.A.base + (long long)mt * p.A.row_tile_stride + (long long)(64 * a + row) * p.A.ld + 16 * chunk
+                      : p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride +
+                            (long long)(64 * b + row - 64) * p.B.ld + 16 * chunk;
+  }
+  const int SS = dg ? kSubStage / 2 : kSubStage;  // ring stage bytes
+  const int NSt = dg ? 2 * kSubStages : kSubStages;
+  auto stage = [&](int st, int buf) {
+    const long long o = (long long)st * kKStepBytes;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < np)
+        __builtin_amdgcn_global_load_lds((const void*)(src[j] + o), (lds_void*)(lds + buf * SS + ldst[j]), 16, 0, 0);
+  };
+  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
+  const int brow = dg ? 0 : 64;  // ring row of B row 0
+  f32x4 acc[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int P = NSt - 1;  // K-steps in flight: 5 (diagonal region) or 2
+  for (int i = 0; i < P; ++i) stage(k0 + i < k1 ? k0 + i : k1 - 1, i);
+  int buf = 0;
+  for (int st = k0; st < k1; ++st) {
+    // own pieces of step st landed (the P - 1 younger steps' np each in flight: 2 x 4 or 4 x 1);
+    // after the barrier every wave's have, and every wave has finished reading the buffer
+    // refilled next (the one read in the previous step)
+    static_assert(kSubStages == 3, "wait counts assume 6- and 3-stage rings");
+    if (dg) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int nb2 = buf == 0 ? NSt - 1 : buf - 1;  // (st + P) % NSt
+    stage(st + P < k1 ? st + P : k1 - 1, nb2);
+    const lds_char* sb = lds + buf * SS;
+    frag af[2], bf[2][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int pch = ((4 * c + cq) ^ sw) << 4;
+      af[c] = *(lds_frag*)(sb + (16 * w + r16) * kKStepBytes + pch);
+#pragma unroll
+      for (int f = 0; f < 4; ++f) bf[c][f] = *(lds_frag*)(sb + (brow + 16 * f + r16) * kKStepBytes + pch);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) acc[f] = MM::mma(af[c], bf[c][f], acc[f]);
+    buf = buf == NSt - 1 ? 0 : buf + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
+  int* flag = reinterpret_cast<int*>(smem + kSubStages * kSubStage + 4 * 64 * 8);
+  int* cnt_pair = p.sk_cnt + 4 * nt_d;  // [nt_d][6] after the [nt_d][4] row-group tickets
+  if (!dg) {
+    // K halves: publish this half's fp32 partial (write-through), the second to arrive adds it
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs + (size_t)((tile * 6 + q) * 2) * 4096, 0,
+                                                      2 * 4096 * 4, 0x00020000);
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[f]), prs,
+                                             (int)((hk * 4096 + ((w * 4 + f) * 64 + lane) * 4) * 4), 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(cnt_pair + tile * 6 + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == 1;
+      if (last) __hip_atomic_store(cnt_pair + tile * 6 + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(((1 - hk) * 4096 + ((w * 4 + f) * 64 + lane) * 4) * 4), 0, 16);
+      acc[f] += __builtin_bit_cast(f32x4, v);  // fp32 addition commutes: either arrival order, same bits
+    }
+  }
+  // lane holds S[row 64a + 16w + 4 (lane >> 4) + r][col 64b + 16 f + (lane & 15)] (tile-local)
+  const int rb0 = 64 * a + 16 * w;
+  if (p.sc) {  // kept cosines of region (a, b), canonical fragment order, before the masks
+    TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
+    if constexpr (sizeof(TS) == 2) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        union { TS h[8]; u32x4 u; } pk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pk.h[r] = from_f32<TS>(acc[2 * h2][r]);
+          pk.h[4 + r] = from_f32<TS>(acc[2 * h2 + 1][r]);
+        }
+        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * h2, lane) * 8) = pk.u;
+      }
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * b + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f];
+    }
+  }
+  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
+  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
+  const float sc_ = p.acc_scale, M = p.y_scale;
+  // masked logits (log2 units)
+  float y[4][4];  // [r][f]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int tr = rb0 + 4 * (lane >> 4) + r, gi = r0 + tr;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int tc = 64 * b + 16 * f + (lane & 15), d = tc - tr;
+      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
+                        ((d == D2) & (gi >= p.n_half));
+      y[r][f] = drop ? kNegInf : acc[f][r] * sc_;
+    }
+  }
+  // row partials of group a over b's 64 columns -> contribution (a, slot b)
+  const auto rrs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + a) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float m = M;
+    if constexpr (!FX) m = row16_max(fmaxf(fmaxf(y[r][0], y[r][1]), fmaxf(y[r][2], y[r][3])));
+    const float ms = (m == kNegInf) ? 0.f : m;
+    float sr = (fast_exp2(y[r][0] - ms) + fast_exp2(y[r][1] - ms)) + (fast_exp2(y[r][2] - ms) + fast_exp2(y[r][3] - ms));
+    sr = row16_sum(sr);
+    const float mo = FX ? (sr > 0.f ? M : kNegInf) : m;
+    if ((lane & 15) == 0)  // write-through: merged by the row group's last contributor on any XCD
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mo), __float_as_uint(sr)}, rrs,
+                                            (b * 64 + 16 * w + 4 * (lane >> 4) + r) * 8, 0, 16);
+  }
+  // column partials of group b over a's 64 rows (off-diagonal regions) -> contribution (b, slot a):
+  // per wave over its 16 rows, then the 4 waves merged in wave order through LDS
+  if (!dg) {
+    typedef __attribute__((address_space(3))) f32x2 lds_f2;
+    lds_f2* xw = (lds_f2*)(lds + kSubStages * kSubStage);  // [4 waves][64 cols]
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      float m = M;
+      if constexpr (!FX) m = xrow_max(fmaxf(fmaxf(y[0][f], y[1][f]), fmaxf(y[2][f], y[3][f])));
+      const float ms = (m == kNegInf) ? 0.f : m;
+      float sc = (fast_exp2(y[0][f] - ms) + fast_exp2(y[1][f] - ms)) + (fast_exp2(y[2][f] - ms) + fast_exp2(y[3][f] - ms));
+      sc = xrow_sum(sc);
+      const float mo = FX ? (sc > 0.f ? M : kNegInf) : m;
+      if (lane < 16) xw[w * 64 + 16 * f + lane] = f32x2{mo, sc};
+    }
+    __syncthreads();
+    if (tid < 64) {
+      f32x2 v = xw[tid];
+      float m = v.x, sm = v.y;
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const f32x2 u = xw[ww * 64 + tid];
+        lse_merge(m, sm, u.x, u.y);
+      }
+      const auto crs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + b) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(m), __float_as_uint(sm)}, crs, (a * 64 + tid) * 8, 0, 16);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {  // one ticket per contributed row group; the 4th contributor merges the group
+    int lastm = 0;
+    const int ga[2] = {a, b};
+    for (int k = 0; k < (dg ? 1 : 2); ++k) {
+      const int old = __hip_atomic_fetch_add(p.sk_cnt + tile * 4 + ga[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == 3) {
+        __hip_atomic_store(p.sk_cnt + tile * 4 + ga[k], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lastm |= 1 << k;
+      }
+    }
+    flag[1] = lastm;
+  }
+  __syncthreads();
+  const int lastm = flag[1];
+  const int k = tid >> 6;  // wave 0 merges group a, wave 1 group b
+  if (k > 1 || !((lastm >> k) & 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  const int g = k == 0 ? a : b;
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + g) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
+  u32x2 qv[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) qv[kk] = __builtin_amdgcn_raw_buffer_load_b64(srs, (kk * 64 + lane) * 8, 0, 16);
+  float m = __uint_as_float(qv[0][0]), sm = __uint_as_float(qv[0][1]);
+#pragma unroll
+  for (int kk = 1; kk < 4; ++kk) lse_merge(m, sm, __uint_as_float(qv[kk][0]), __uint_as_float(qv[kk][1]));
+  p.part[(long long)nt * p.Rpad + r0 + 64 * g + lane] = make_float2(m, sm);
 }
 
 // ------------------------------------------------------------------------------------

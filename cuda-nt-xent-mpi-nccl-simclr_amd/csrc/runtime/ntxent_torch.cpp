@@ -215,8 +215,12 @@ at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at
   return zqt;
 }
 
+// zero_cos: the raw op (Python fwd_stats) returns zeros in the lower 64x64 regions of diagonal
+// tiles, which the forward may leave unwritten (the coefficient pass mirrors them from the upper
+// ones, diag_up_kernel); the training path keeps the buffer uninitialised (a 66 MiB memset per
+// step at the headline otherwise)
 std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P,
-                                  bool keep_cos) {
+                                  bool keep_cos, bool zero_cos = false) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   NTXENT_CHECK(zq_all.size(0) == (long)P.g.world * P.g.rows_pad && zq_all.size(1) == P.op_ld(),
@@ -224,7 +228,9 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
   const at::DeviceGuard guard(zq_local.device());
   auto part = at::empty({P.g.col_tiles, P.g.rows_pad, 2}, opts(zq_local, at::kFloat));
   at::Tensor sc;
-  if (keep_cos) sc = at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
+  if (keep_cos)
+    sc = zero_cos ? at::zeros({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())))
+                  : at::empty({(long)P.n_fwd * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   auto ws = gemm_ws(zq_local, P.n_fwd, P);
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd,
@@ -944,7 +950,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"));
-  m.def("fwd_stats", &fwd_stats, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"));
+  m.def("fwd_stats", [](const at::Tensor& zl, const at::Tensor& za, const Plan& P, bool keep) {
+    return fwd_stats(zl, za, P, keep, true);
+  }, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"));
   m.def("lse", &lse, py::arg("part"), py::arg("ypos"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
         py::arg("zq") = py::none(), py::arg("zqt") = py::none());
   m.def("coef", [](const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
@@ -962,6 +970,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fwd_stream_enabled", &ntxent::fwd_stream_enabled);
   m.def("set_splitk_piece_major", &ntxent::set_splitk_piece_major, py::arg("on"));
   m.def("splitk_piece_major", &ntxent::splitk_piece_major);
+  m.def("set_diag_upper", &ntxent::set_diag_upper, py::arg("on"));
+  m.def("diag_upper_enabled", &ntxent::diag_upper_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
   m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);

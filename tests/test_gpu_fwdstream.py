@@ -96,3 +96,39 @@ def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
     if compute != "fp8":
         lo, _ = _oracle(h, 0.07)
         assert abs(la - lo) <= 2e-4 * abs(lo)
+
+
+@pytest.mark.parametrize("rows,dim,compute,T", [
+    (8192, 2048, "fp16", 0.07),   # headline: 16 diagonal tiles in the remainder
+    (16384, 1024, "bf16", 0.07),  # config 5 shape: 32 diagonal tiles (2 blocks per CU)
+    (8192, 1024, "fp32", 0.07),   # f32 kept cosines
+    (8192, 1024, "fp16", 0.02),   # per-tile-max epilogue (no fixed shift)
+])
+def test_diag_upper_matches_full_subtiles(ext, rows, dim, compute, T):
+    """The forward's diagonal remainder from the upper 64x64 regions only (diag_up_kernel; the
+    coefficient pass mirrors the rest) against all 16 regions over the whole K (diag_sub_kernel):
+    partials to fp32 rounding (the off-diagonal regions sum two K halves), loss and gradient."""
+    import ntxent_amd
+
+    _, h = _inputs(rows, dim, torch.float32 if compute == "fp32" else torch.bfloat16, seed=43)
+    plan = ext.get_plan(rows, dim, 1, 0, T, compute, 0)
+    zq, inv, ypos, _ = ext.prep(h, plan)
+    old = ext.diag_upper_enabled()
+    outs = {}
+    try:
+        for up in (True, False):
+            ext.set_diag_upper(up)
+            part, _ = ext.fwd_stats(zq, zq, plan, True)
+            x = h.clone().requires_grad_(True)
+            loss = ntxent_amd.ntxent_loss(x, T, compute=compute)
+            (g,) = torch.autograd.grad(loss, x)
+            torch.cuda.synchronize()
+            outs[up] = (part.clone(), loss.item(), g.float())
+    finally:
+        ext.set_diag_upper(old)
+    (pa, la, ga), (pb, lb, gb) = outs[True], outs[False]
+    # (max, sum) partials: same max (fixed shift) / sums to fp32 rounding
+    torch.testing.assert_close(pa, pb, rtol=2e-5, atol=0)
+    assert abs(la - lb) <= 2e-6 * abs(lb)
+    scale = gb.abs().max().item()
+    assert (ga - gb).abs().max().item() <= 4e-3 * scale

@@ -43,6 +43,18 @@ def nccl_group():
     dist.destroy_process_group()
 
 
+def _upper_cosines(sc, rows):
+    """Kept cosines (16-bit canonical fragment order) with the lower 64x64 regions of the own
+    block's diagonal tiles (the last rows / 256 tiles) zeroed."""
+    rt = (rows + 255) // 256
+    t = sc.float().view(-1, 16, 8, 512).clone()  # [tile][16-row block][32-col pair][lane * 8]
+    i = torch.arange(16, device=sc.device).view(16, 1)
+    j = torch.arange(8, device=sc.device).view(1, 8)
+    lower = (i >> 2) > (j >> 1)
+    t[-rt:][:, lower] = 0
+    return t
+
+
 def test_p2p_batch_self_send_recv(nccl_group):
     from ntxent_amd.parallel.symmetric import _p2p
 
@@ -88,7 +100,11 @@ def test_comm_overlap_reserve_is_bitwise_neutral(nccl_group, ext):
             assert torch.equal(dst, big)
     a, b, c = outs[(0, False)], outs[(reserve, False)], outs[(reserve, True)]
     assert torch.equal(b[0], c[0]) and torch.equal(b[1], c[1])
-    assert torch.equal(a[1], b[1])  # the kept cosines do not depend on the schedule
+    # the kept cosines do not depend on the schedule beyond rounding: the reserve moves diagonal
+    # tiles between the whole-tile GEMM and the remainder kernel, which sums two K halves of the
+    # upper regions and leaves the lower ones (mirrored by the coefficient pass) unwritten
+    ka, kb = _upper_cosines(a[1], rows), _upper_cosines(b[1], rows)
+    torch.testing.assert_close(ka, kb, rtol=0, atol=1e-3)
     torch.testing.assert_close(a[0], b[0], rtol=1e-5, atol=0)
 
 
