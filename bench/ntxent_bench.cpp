@@ -363,6 +363,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-fwd-stream") ntxent::set_fwd_stream(false);
     else if (a == "--no-sk-pm") ntxent::set_splitk_piece_major(false);
     else if (a == "--no-diag-up") ntxent::set_diag_upper(false);
+    else if (a == "--zorder") ntxent::set_superblock_order(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "--negatives") {
@@ -388,7 +389,8 @@ int main(int argc, char** argv) {
                   "  --no-fwd-stream: forward GEMM drains after each item and issues the next item's prologue\n"
                   "              after its epilogue (A/B; default: the operand streams run into the next item)\n"
                   "  --no-sk-pm: split-K forward with the tile-major straddling pieces (A/B; default piece-major)\n"
-                  "  --no-diag-up: diagonal remainder over all 16 sub-tiles (A/B; default: upper regions only)\n");
+                  "  --no-diag-up: diagonal remainder over all 16 sub-tiles (A/B; default: upper regions only)\n"
+                  "  --zorder: own-block tiles in Z-order (A/B; default: 8-panel superblocks)\n");
       return 0;
     }
   }

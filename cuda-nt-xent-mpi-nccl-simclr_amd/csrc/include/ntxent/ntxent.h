@@ -258,6 +258,9 @@ bool splitk_piece_major();
 // (diag_up_kernel; default on; off: all 16 regions over the whole K, diag_sub_kernel)
 void set_diag_upper(bool on);
 bool diag_upper_enabled();
+// Own-block tile order (plans built afterwards): 8-panel superblocks (default) or Z-order (A/B)
+void set_superblock_order(bool on);
+bool superblock_order_enabled();
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad

@@ -972,6 +972,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_piece_major", &ntxent::splitk_piece_major);
   m.def("set_diag_upper", &ntxent::set_diag_upper, py::arg("on"));
   m.def("diag_upper_enabled", &ntxent::diag_upper_enabled);
+  m.def("set_superblock_order", &ntxent::set_superblock_order, py::arg("on"));
+  m.def("superblock_order_enabled", &ntxent::superblock_order_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
   m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);
