@@ -95,9 +95,11 @@ static at::Tensor upload_tiles(const std::vector<int4>& v, int device) {
 std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double temperature,
                                const std::string& compute, int device) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, float, int, int>, std::shared_ptr<Plan>> cache;
+  static std::map<std::tuple<int, int, int, int, float, int, int, int>, std::shared_ptr<Plan>> cache;
   const DType comp = choose_compute(at::kFloat, compute != "fp32" && compute != "float32", compute);
-  auto key = std::make_tuple(rows, dim, world, rank, (float)temperature, (int)comp, device);
+  // the tile order is part of the plan (its tile lists): a toggled order gets its own plan
+  auto key = std::make_tuple(rows, dim, world, rank, (float)temperature, (int)comp, device,
+                             (int)superblock_order_enabled());
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;

@@ -132,3 +132,27 @@ def test_diag_upper_matches_full_subtiles(ext, rows, dim, compute, T):
     assert abs(la - lb) <= 2e-6 * abs(lb)
     scale = gb.abs().max().item()
     assert (ga - gb).abs().max().item() <= 4e-3 * scale
+
+
+@pytest.mark.parametrize("rows,dim,compute", [(8192, 2048, "fp16"), (16384, 1024, "bf16")])
+def test_superblock_order_bitwise(ext, rows, dim, compute):
+    """Own-block tiles in 8-panel superblocks (default) vs Z-order: every tile's work and every
+    merge order (partials per column tile, coefficient tiles by slot) are independent of the list
+    order, so loss and gradient agree bitwise (the order is part of the plan-cache key)."""
+    import ntxent_amd
+
+    _, h = _inputs(rows, dim, torch.bfloat16, seed=53)
+    old = ext.superblock_order_enabled()
+    outs = {}
+    try:
+        for sb in (True, False):
+            ext.set_superblock_order(sb)
+            x = h.clone().requires_grad_(True)
+            loss = ntxent_amd.ntxent_loss(x, 0.07, compute=compute)
+            (g,) = torch.autograd.grad(loss, x)
+            torch.cuda.synchronize()
+            outs[sb] = (loss.detach(), g)
+    finally:
+        ext.set_superblock_order(old)
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
