@@ -200,6 +200,10 @@ def run_rank(a) -> None:
     if world > 1:
         kw = {"timeout": timedelta(seconds=a.timeout)}
         if backend == "nccl":
+            if a.share_gpu:  # RCCL rehearsal on one GPU: per-rank host ids, socket transport
+                from ntxent_amd.parallel.commstats import rccl_shared_gpu_env
+
+                rccl_shared_gpu_env(rank)
             dist.init_process_group("nccl", device_id=dev, **kw)
         else:
             dist.init_process_group("gloo", **kw)

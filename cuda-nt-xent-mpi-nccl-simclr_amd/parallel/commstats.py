@@ -93,6 +93,23 @@ def comm_overlap(cus: int):
         C.set_grid_reserve(old)
 
 
+def rccl_shared_gpu_env(rank: int) -> Dict[str, str]:
+    """Environment for rehearsing W RCCL ranks on ONE GPU (call before init_process_group).
+
+    RCCL refuses two ranks of one host on one device ("Duplicate GPU detected"). A distinct
+    ``NCCL_HOSTID`` per rank makes each rank its own host for RCCL's topology, so the ranks
+    connect over RCCL's socket transport on loopback instead of xGMI P2P: the same RCCL
+    collectives, grouped send/recv, proxy threads and communicator streams run as on an 8-GPU
+    node, only the wire differs (and so the timing means nothing). Existing settings win."""
+    import os
+
+    env = {"NCCL_HOSTID": f"ntxent-shared-gpu-rank{int(rank)}", "NCCL_SOCKET_IFNAME": "lo",
+           "NCCL_IB_DISABLE": "1"}
+    for k, v in env.items():
+        os.environ.setdefault(k, v)
+    return {k: os.environ[k] for k in env}
+
+
 def use_compute_stream(device=None, priority: str = "high"):
     """Make a new (high-priority by default) stream the current stream of `device` and return
     it. Data-parallel steps should not run on the device's default stream: there the RCCL

@@ -1,9 +1,9 @@
 """The real torch.distributed path (DistNTXentFunction: async gathers, own-tile / remote-tile
 overlap, LSE all-gather, loss all-reduce, rank-local symmetric backward) with W processes.
 
-RCCL needs one GPU per rank, so on a 1-GPU box the W ranks share cuda:0 and talk over gloo
-(its collectives stage GPU tensors through the host); every HIP kernel, plan and buffer is the
-one a W-GPU RCCL run uses. Results are checked against the fp64 oracle on the gathered batch.
+On a 1-GPU box the W ranks share cuda:0 and talk over gloo (its collectives stage GPU tensors
+through the host) or over RCCL itself (per-rank host ids, RCCL's socket transport); every HIP
+kernel, plan and buffer is the one a W-GPU RCCL run uses. Results are checked against the fp64 oracle on the gathered batch.
 """
 import os
 import socket
@@ -33,16 +33,22 @@ def _shards(W, n, dim, seed):
     return out
 
 
-def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives="allgather"):
+def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives="allgather", backend="gloo"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=W)
+    torch.cuda.set_device(0)
+    if backend == "nccl":
+        from ntxent_amd.parallel.commstats import rccl_shared_gpu_env
+
+        rccl_shared_gpu_env(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=W, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=W)
     try:
         from ntxent_amd.parallel import dist_ntxent_loss
 
-        torch.cuda.set_device(0)
         h = _shards(W, n, dim, seed=11)[rank].float().cuda().requires_grad_(True)
         loss = dist_ntxent_loss(h, T, compute=compute, keep_logits=keep, overlap=overlap, backward_mode=mode,
                                 negatives=negatives)
@@ -68,11 +74,33 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives
     (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric"),  # 16 row tiles: 4 exchange chunks
 ])
 def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
+    _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "gloo")
+
+
+# RCCL itself at W > 1 on the 1-GPU box: per-rank NCCL_HOSTID makes RCCL accept two ranks on one
+# device and connect them over its socket transport (commstats.rccl_shared_gpu_env), so the
+# grouped batch_isend_irecv of the symmetric mode, the async all-gathers / reduce-scatter of the
+# all-gather mode and the ring's exchanges run through RCCL's communicator and kernels, with the
+# GEMMs' comm CU reserve active (only the wire is not xGMI).
+@pytest.mark.parametrize("W,n,dim,compute,keep,overlap,mode,negatives", [
+    (2, 512, 128, "fp16", False, True, "symmetric", "symmetric"),
+    (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric"),
+    (3, 384, 80, "fp32", True, True, "symmetric", "symmetric"),
+    (2, 300, 96, "fp16", False, True, "symmetric", "allgather"),
+    (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather"),
+    (2, 256, 128, "fp16", False, True, "symmetric", "ring"),
+])
+def test_multiprocess_rccl_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
+    _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "nccl")
+
+
+def _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, backend):
     T = 0.1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives))
+    procs = [ctx.Process(target=_worker, args=(r, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives,
+                                               backend))
              for r in range(W)]
     for p in procs:
         p.start()
