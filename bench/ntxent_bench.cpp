@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -266,6 +267,12 @@ struct Options {
   int small_splits = 0;
   Negatives negatives = Negatives::kSymmetric;
   bool emulate = false;  // --gpus N as N emulated ranks on GPU 0 (ThreadComm), not N GPUs over RCCL
+  // one rank per PROCESS (--proc-rank r of --gpus N): the RCCL unique id goes through uid_file;
+  // --shared-gpu puts every rank on GPU 0 (launch each with its own NCCL_HOSTID: RCCL then
+  // connects them over its socket transport, tools/cpp_rccl_procs.py)
+  int proc_rank = -1;
+  std::string uid_file;
+  bool shared_gpu = false;
 };
 
 // Minimal reusable thread barrier (C++17).
@@ -331,6 +338,41 @@ int run_multi(const Options& o, DType in, DType comp) {
   return 0;
 }
 
+// One rank of a multi-process data-parallel run (the native counterpart of the torchrun path):
+// rank 0 publishes the RCCL unique id through a file (written, then renamed), the others wait
+// for it. Each rank prints its loss and mean fwd+bwd time; the launcher compares the ranks' loss
+// with the --emulate run of the same seeds.
+int run_proc(const Options& o, DType in, DType comp) {
+  const int N = o.gpus, r = o.proc_rank;
+  NTXENT_CHECK(r >= 0 && r < N && !o.uid_file.empty(), "--proc-rank needs 0 <= r < --gpus and --uid-file");
+  std::string uid;
+  if (r == 0) {
+    uid = RcclComm::unique_id();
+    const std::string tmp = o.uid_file + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    NTXENT_CHECK(f && std::fwrite(uid.data(), 1, uid.size(), f) == uid.size(), "cannot write the uid file");
+    std::fclose(f);
+    NTXENT_CHECK(std::rename(tmp.c_str(), o.uid_file.c_str()) == 0, "cannot publish the uid file");
+  } else {
+    for (int t = 0; t < 1200 && uid.size() != RcclComm::kIdBytes; ++t) {
+      if (FILE* f = std::fopen(o.uid_file.c_str(), "rb")) {
+        char b[RcclComm::kIdBytes];
+        if (std::fread(b, 1, sizeof(b), f) == sizeof(b)) uid.assign(b, sizeof(b));
+        std::fclose(f);
+      }
+      if (uid.size() != RcclComm::kIdBytes) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    NTXENT_CHECK(uid.size() == RcclComm::kIdBytes, "timed out waiting for the uid file");
+  }
+  RcclComm comm(r, N, uid, o.shared_gpu ? 0 : r);
+  Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, &comm, 1234 + r, true, 0, o.negatives);
+  const Result fb = stats(bench.time(o.graph ? 3 : 2, o.warmup, o.iters));
+  std::printf("proc rank %d/%d B/rank=%d D=%d %s %s: fwd+bwd %.4f ms, loss %.6f\n", r, N, o.batch, o.dim,
+              o.dtype.c_str(), o.negatives == Negatives::kSymmetric ? "symmetric" : "allgather", fb.mean,
+              bench.loss());
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -372,6 +414,9 @@ int main(int argc, char** argv) {
       o.negatives = v == "symmetric" ? Negatives::kSymmetric : Negatives::kAllGather;
     }
     else if (a == "--emulate") o.emulate = true;
+    else if (a == "--proc-rank") o.proc_rank = std::stoi(next());
+    else if (a == "--uid-file") o.uid_file = next();
+    else if (a == "--shared-gpu") o.shared_gpu = true;
     else if (a == "--small-fuse-rows") ntxent::set_small_fuse_rows(std::stoi(next()));
     else if (a == "-h" || a == "--help") {
       std::printf("usage: ntxent_bench [--batch B --dim D] [--dtype bf16|fp16|fp32] [--compute auto|fp16|bf16|fp32|fp8]\n"
@@ -380,6 +425,7 @@ int main(int argc, char** argv) {
                   "  --no-small: large-problem pipeline for every shape (no one-launch small path)\n"
                   "  --gpus N [--negatives symmetric|allgather] [--emulate]: data parallel over N GPUs (RCCL),\n"
                   "           or N emulated ranks on GPU 0 (in-process ThreadComm, --emulate)\n"
+                  "  --gpus N --proc-rank r --uid-file F [--shared-gpu]: rank r of N processes over RCCL\n"
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"
@@ -404,6 +450,7 @@ int main(int argc, char** argv) {
   if (o.gpus > 1) {
     if (o.batch <= 0) o.batch = 4096;
     if (o.dim <= 0) o.dim = 2048;
+    if (o.proc_rank >= 0) return run_proc(o, in, comp);
     return run_multi(o, in, comp);
   }
 
