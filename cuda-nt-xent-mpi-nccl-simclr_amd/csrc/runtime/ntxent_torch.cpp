@@ -24,6 +24,7 @@
 #include <tuple>
 #include <vector>
 
+#include "ntxent/engine.h"
 #include "ntxent/ntxent.h"
 
 namespace ntxent {
@@ -890,6 +891,116 @@ bool check_tensor_core_support() {
   return check_matrix_core_support(dev);
 }
 
+
+// ---- the native Engine from Python (ntxent_amd.native) ------------------------------------
+// The libtorch-free runtime (engine.h: one arena, fixed launch sequence, hipGraph capture,
+// RcclComm data parallelism) driven from torch tensors on the current stream. The RCCL unique
+// id is produced by rccl_unique_id() on one rank and handed to the others by the caller
+// (ntxent_amd.native bootstraps it through the torch.distributed store).
+namespace {
+DType parse_dtype_name(const std::string& s) {
+  if (s == "float32" || s == "fp32") return DType::F32;
+  if (s == "float16" || s == "fp16") return DType::F16;
+  if (s == "bfloat16" || s == "bf16") return DType::BF16;
+  if (s == "fp8" || s == "e4m3") return DType::FP8;
+  throw std::invalid_argument("unknown dtype '" + s + "' (fp32|fp16|bf16|fp8)");
+}
+at::ScalarType scalar_of(DType t) {
+  return t == DType::F32 ? at::kFloat : (t == DType::F16 ? at::kHalf : at::kBFloat16);
+}
+
+class NativeEngine {
+ public:
+  NativeEngine(int rows, int dim, double T, const std::string& input, const std::string& compute,
+               const std::string& negatives, int rank, int world, const std::string& uid, int device, bool keep_cos,
+               int comm_reserve_cus)
+      : device_(device) {
+    NTXENT_CHECK(world >= 1 && rank >= 0 && rank < world, "NativeEngine: bad rank/world");
+    NTXENT_CHECK(negatives == "symmetric" || negatives == "allgather", "negatives must be symmetric|allgather");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
+    if (world > 1) comm_ = std::make_unique<RcclComm>(rank, world, uid, device);
+    EngineConfig cfg;
+    cfg.rows = rows;
+    cfg.dim = dim;
+    cfg.temperature = (float)T;
+    cfg.input = parse_dtype_name(input);
+    NTXENT_CHECK(cfg.input != DType::FP8, "NativeEngine: input must be fp32|fp16|bf16");
+    cfg.compute = compute == "auto" ? (cfg.input == DType::F32 ? DType::F32 : DType::F16) : parse_dtype_name(compute);
+    cfg.keep_cos = keep_cos;
+    cfg.comm_reserve_cus = comm_reserve_cus;
+    cfg.negatives = negatives == "symmetric" ? Negatives::kSymmetric : Negatives::kAllGather;
+    cfg.device = device;
+    in_ = scalar_of(cfg.input);
+    eng_ = std::make_unique<Engine>(cfg, comm_.get());
+  }
+
+  void forward(const at::Tensor& h) {
+    check_h(h);
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    h_ = h;  // the backward reads the forward's h
+    eng_->forward(h.data_ptr(), cur_stream(h));
+  }
+  at::Tensor backward(const c10::optional<at::Tensor>& grad_out) {
+    NTXENT_CHECK(h_.defined(), "NativeEngine.backward needs a preceding forward");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    at::Tensor go;
+    if (grad_out && grad_out->defined()) {
+      go = grad_out->to(h_.device(), at::kFloat).reshape({1}).contiguous();
+    }
+    at::Tensor dh = at::empty_like(h_);
+    eng_->backward(go.defined() ? go.data_ptr<float>() : nullptr, dh.data_ptr(), cur_stream(h_));
+    return dh;
+  }
+  // the global mean loss as a 0-d fp32 tensor (stream-ordered copy of the engine's slot)
+  at::Tensor loss_tensor() const {
+    NTXENT_CHECK(h_.defined(), "no forward yet");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    at::Tensor out = at::empty({}, h_.options().dtype(at::kFloat));
+    NTXENT_HIP_CHECK(hipMemcpyAsync(out.data_ptr(), eng_->loss_device(), sizeof(float), hipMemcpyDeviceToDevice,
+                                    cur_stream(h_)));
+    return out;
+  }
+  std::tuple<at::Tensor, at::Tensor> step(const at::Tensor& h) {
+    forward(h);
+    at::Tensor dh = backward(c10::nullopt);
+    return {loss_tensor(), dh};
+  }
+  // hipGraph of one step for fixed h (dh is returned and reused by every replay)
+  at::Tensor capture(const at::Tensor& h) {
+    check_h(h);
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    h_ = h;
+    gdh_ = at::empty_like(h);
+    eng_->capture(h.data_ptr(), gdh_.data_ptr(), cur_stream(h));
+    return gdh_;
+  }
+  void replay() {
+    NTXENT_CHECK(eng_->captured(), "NativeEngine.replay needs capture()");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
+    eng_->replay(cur_stream(h_));
+  }
+  size_t device_bytes() const { return eng_->device_bytes(); }
+  bool symmetric() const { return eng_->symmetric(); }
+  bool small() const { return eng_->small(); }
+  int rank() const { return comm_ ? comm_->rank() : 0; }
+  int world() const { return comm_ ? comm_->world() : 1; }
+
+ private:
+  void check_h(const at::Tensor& h) const {
+    const auto& c = eng_->config();
+    NTXENT_CHECK(h.is_cuda() && h.device().index() == device_, "h must be on the engine's device");
+    NTXENT_CHECK(h.scalar_type() == in_, "h dtype does not match the engine's input dtype");
+    NTXENT_CHECK(h.dim() == 2 && h.size(0) == c.rows && h.size(1) == c.dim && h.is_contiguous(),
+                 "h must be a contiguous [rows, dim] tensor");
+  }
+  int device_ = 0;
+  at::ScalarType in_ = at::kBFloat16;
+  std::unique_ptr<RcclComm> comm_;  // declared before eng_: destroyed after it
+  std::unique_ptr<Engine> eng_;
+  at::Tensor h_, gdh_;
+};
+}  // namespace
+
 }  // namespace th
 }  // namespace ntxent
 
@@ -942,6 +1053,25 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("dz_sym", &Plan::dz_sym)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
+  py::class_<NativeEngine>(m, "NativeEngine")
+      .def(py::init<int, int, double, const std::string&, const std::string&, const std::string&, int, int,
+                    const std::string&, int, bool, int>(),
+           py::arg("rows"), py::arg("dim"), py::arg("temperature"), py::arg("input") = "bf16",
+           py::arg("compute") = "auto", py::arg("negatives") = "symmetric", py::arg("rank") = 0, py::arg("world") = 1,
+           py::arg("uid") = std::string(), py::arg("device") = 0, py::arg("keep_cos") = true,
+           py::arg("comm_reserve_cus") = 8)
+      .def("forward", &NativeEngine::forward, py::arg("h"))
+      .def("backward", &NativeEngine::backward, py::arg("grad_out") = py::none())
+      .def("loss_tensor", &NativeEngine::loss_tensor)
+      .def("step", &NativeEngine::step, py::arg("h"))
+      .def("capture", &NativeEngine::capture, py::arg("h"))
+      .def("replay", &NativeEngine::replay)
+      .def_property_readonly("device_bytes", &NativeEngine::device_bytes)
+      .def_property_readonly("symmetric", &NativeEngine::symmetric)
+      .def_property_readonly("small", &NativeEngine::small)
+      .def_property_readonly("rank", &NativeEngine::rank)
+      .def_property_readonly("world", &NativeEngine::world);
+  m.def("rccl_unique_id", []() { return py::bytes(ntxent::RcclComm::unique_id()); });
   m.def("get_plan", &get_plan, py::arg("rows"), py::arg("dim"), py::arg("world"), py::arg("rank"),
         py::arg("temperature"), py::arg("compute"), py::arg("device"));
   m.def("choose_compute", [](const std::string& in_dtype, bool mp, const std::string& ov) {

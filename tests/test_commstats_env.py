@@ -24,3 +24,13 @@ def test_comm_reserve_defaults(monkeypatch):
     assert comm_reserve_cus("nccl") == 8
     monkeypatch.setenv("NTXENT_COMM_RESERVE_CUS", "16")
     assert comm_reserve_cus("nccl") == 16
+
+
+def test_native_engine_rejects_bad_dtype_before_loading():
+    import pytest
+    import torch
+
+    from ntxent_amd.parallel.native import NativeNTXent
+
+    with pytest.raises(TypeError):
+        NativeNTXent(64, 32, dtype=torch.int8)
