@@ -67,7 +67,7 @@ def parse(argv=None):
     ap.add_argument("--data", default="views", choices=["views", "iid"],
                     help="views: two noisy views of a shared random-normal basis (positives correlated, "
                          "as from a SimCLR encoder); iid: independent random-normal rows")
-    ap.add_argument("--impl", default="fused", choices=["fused", "torch"],
+    ap.add_argument("--impl", default="fused", choices=["fused", "native", "torch"],
                     help="torch: unfused PyTorch NT-Xent (hipBLASLt GEMM + eager softmax / cross-entropy, "
                          "the reference's cuBLAS-GEMM + row-kernel design) as an on-device baseline; 1 GPU")
     ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
@@ -226,6 +226,13 @@ def run_rank(a) -> None:
 
     if a.impl == "torch" and world > 1:
         raise SystemExit("--impl torch is a single-GPU baseline")
+    if a.impl == "native":
+        if not on_gpu or a.graph or (world > 1 and a.negatives == "ring"):
+            raise SystemExit("--impl native: GPU only, no --graph, negatives symmetric|allgather")
+        if world > 1 and a.share_gpu:  # the Engine's own RcclComm on one GPU (socket transport)
+            from ntxent_amd.parallel.commstats import rccl_shared_gpu_env
+
+            rccl_shared_gpu_env(rank)
     R = 2 * a.batch
 
     def make_input(dtype):
@@ -240,6 +247,14 @@ def run_rank(a) -> None:
 
     def make_step(h, compute):
         one = torch.ones((), device=dev, dtype=torch.float32 if h.dtype != torch.float64 else h.dtype)
+        if a.impl == "native":  # the C++ Engine (+ its own RcclComm at N > 1), no autograd graph
+            from ntxent_amd.parallel.native import NativeNTXent
+
+            hd = h.detach()
+            kw = dict(dtype=hd.dtype, compute=compute, negatives=a.negatives, keep_cos=not a.recompute)
+            eng = (NativeNTXent.from_process_group(R, a.dim, a.temperature, **kw) if world > 1
+                   else NativeNTXent(R, a.dim, a.temperature, **kw))
+            return lambda: eng.step(hd)
 
         def step():
             if a.impl == "torch":
@@ -389,6 +404,7 @@ def run_rank(a) -> None:
             "config": {
                 "model": ("NT-Xent loss (SimCLR), torch CPU path (plumbing only)" if not on_gpu
                           else "NT-Xent loss (SimCLR), fused MFMA fwd+bwd" if a.impl == "fused"
+                          else "NT-Xent loss (SimCLR), fused MFMA fwd+bwd, native C++ Engine" if a.impl == "native"
                           else "NT-Xent loss (SimCLR), unfused PyTorch baseline (hipBLASLt + eager)"),
                 "global_batch": world * a.batch,
                 "seq_len": None,
