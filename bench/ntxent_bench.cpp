@@ -404,6 +404,8 @@ int main(int argc, char** argv) {
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
     else if (a == "--no-fwd-stream") ntxent::set_fwd_stream(false);
     else if (a == "--no-sk-pm") ntxent::set_splitk_piece_major(false);
+    else if (a == "--no-sk-half") ntxent::set_splitk_half(false);
+    else if (a == "--no-sk-dz-half") ntxent::set_splitk_dz_half(false);
     else if (a == "--no-diag-up") ntxent::set_diag_upper(false);
     else if (a == "--zorder") ntxent::set_superblock_order(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
@@ -435,6 +437,8 @@ int main(int argc, char** argv) {
                   "  --no-fwd-stream: forward GEMM drains after each item and issues the next item's prologue\n"
                   "              after its epilogue (A/B; default: the operand streams run into the next item)\n"
                   "  --no-sk-pm: split-K forward with the tile-major straddling pieces (A/B; default piece-major)\n"
+                  "  --no-sk-half: fp32 split-K forward slabs (A/B; default fp16 for 2-byte plans)\n"
+                  "  --no-sk-dz-half: fp32 split-K dZ slabs (A/B; default fp16 for 2-byte plans)\n"
                   "  --no-diag-up: diagonal remainder over all 16 sub-tiles (A/B; default: upper regions only)\n"
                   "  --zorder: own-block tiles in Z-order (A/B; default: 8-panel superblocks)\n");
       return 0;

@@ -254,6 +254,13 @@ bool fwd_stream_enabled();
 // (default on; off: the flattened tile-major split with straddling pieces, for A/B)
 void set_splitk_piece_major(bool on);
 bool splitk_piece_major();
+// piece-major split-K forward of fp16/bf16 plans: pieces publish fp16 partial tiles (default
+// on; off: fp32 slabs, twice the bytes written by the GEMM and read by sk_reduce_kernel)
+void set_splitk_half(bool on);
+bool splitk_half();
+// the same for the split-K dZ (sk_dz_reduce_kernel)
+void set_splitk_dz_half(bool on);
+bool splitk_dz_half();
 // Diagonal remainder of the forward: upper 64x64 regions only, K halves for the off-diagonal ones
 // (diag_up_kernel; default on; off: all 16 regions over the whole K, diag_sub_kernel)
 void set_diag_upper(bool on);

@@ -1085,6 +1085,8 @@ static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in th
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
 static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
 static std::atomic<bool> g_sk_piece_major{true};  // split-K forward: tile-aligned pieces, piece-major blocks
+static std::atomic<bool> g_sk_half{true};        // piece-major split-K forward of 2-byte plans: fp16 slabs
+static std::atomic<bool> g_sk_dz_half{true};     // piece-major split-K dZ of 2-byte plans: fp16 slabs
 static std::atomic<bool> g_diag_up{true};        // diagonal remainder: upper regions only (diag_up_kernel)
 static std::atomic<bool> g_sb_order{true};       // own-block tile order in 8-panel superblocks (own_block_tiles)
 void set_diag_subtiles(bool on) { g_diag_sub = on; }
@@ -1106,6 +1108,10 @@ void set_dz_sym(bool on) { g_dz_sym = on; }
 bool dz_sym_enabled() { return g_dz_sym.load(); }
 void set_fwd_stream(bool on) { g_fwd_stream = on; }
 void set_splitk_piece_major(bool on) { g_sk_piece_major = on; }
+void set_splitk_half(bool on) { g_sk_half = on; }
+bool splitk_half() { return g_sk_half.load(); }
+void set_splitk_dz_half(bool on) { g_sk_dz_half = on; }
+bool splitk_dz_half() { return g_sk_dz_half.load(); }
 void set_diag_upper(bool on) { g_diag_up = on; }
 void set_superblock_order(bool on) { g_sb_order = on; }
 bool superblock_order_enabled() { return g_sb_order.load(); }
@@ -1174,6 +1180,9 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
       // every K range of a few tiles (profiles/r3/splitk_pm)
       p.sk_out = 2;
       grid = (int)((nk_tile + p.ipb - 1) / p.ipb) * ntiles;
+      // fp16 partial tiles for 2-byte plans: the pieces are normalised-row dot products over a
+      // K range (|x| <= 1), summed in fp32 by the reduce; the kept cosines are 2-byte anyway
+      p.sk_half = (comp == DType::F16 || comp == DType::BF16) && g_sk_half.load() ? 1 : 0;
     } else {
       p.sk_out = 1;
       grid = (int)(((long long)ntiles * nk_tile + p.ipb - 1) / p.ipb);
@@ -1409,6 +1418,9 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     if (splitk_piece_major()) {  // as the forward's: an XCD streams one K range of every panel
       p.sk_out = 2;
       grid = (int)((nk + p.ipb - 1) / p.ipb) * ntiles;
+      // fp16 partial tiles for 2-byte plans (summed in fp32 by sk_dz_reduce_kernel, whose output
+      // is rounded to fp16 / the input dtype anyway)
+      p.sk_half = (comp == DType::F16 || comp == DType::BF16) && g_sk_dz_half.load() ? 1 : 0;
     } else {
       p.sk_out = 1;
       grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);

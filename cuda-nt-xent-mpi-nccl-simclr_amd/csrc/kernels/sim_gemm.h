@@ -107,6 +107,9 @@ struct SimParams {
                          // (2: tile-aligned pieces of ipb K-steps, piece-major: block b = piece
                          // (b / sk_tiles) of tile (b % sk_tiles), slab slot 2 b + 1)
                          // sums a tile's slabs and runs its epilogue in row / column strips
+  int sk_half;           // piece-major split-K (sk_out == 2) of a 2-byte plan: fp16 partial tiles,
+                         // half the slab bytes written and re-read (sk_fixup: fragment pairs of a
+                         // lane in 16-B units)
 };
 
 // Kept-cosine layout for 2-byte types: one 16-byte unit per lane holds the fragments of the
@@ -482,7 +485,22 @@ __device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[8][4], const SimParams& p,
   };
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
   const unsigned lane_off = (unsigned)((w * 32 * 64 + lane) * 16);
-  {
+  if (p.sk_half) {
+    // fp16 partials (the reduce launch sums them in fp32; forward and dZ split-K): fragments
+    // 2q, 2q + 1 of a lane (same mi, ni pair) share one 16-B unit, ((w * 16 + q) * 64 + lane)
+    const unsigned mine = slot_off(bid) + (unsigned)((w * 16 * 64 + lane) * 16);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const f32x4 a = acc[q >> 1][2 * (q & 1)], b = acc[q >> 1][2 * (q & 1) + 1];
+      union { _Float16 h[8]; u32x4 u; } pk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pk.h[r] = (_Float16)a[r];
+        pk.h[4 + r] = (_Float16)b[r];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(pk.u, srs, (int)(mine + q * 64 * 16), 0, 16);
+    }
+  } else {
     const unsigned mine = slot_off(bid) + lane_off;
 #pragma unroll
     for (int f = 0; f < 32; ++f) {
@@ -1928,6 +1946,40 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
     const bool first_partial = (st / nk == tile) && (st % nk != 0);
     return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
   };
+  if (pm && p.sk_half) {
+    // fp16 slabs (sk_fixup): fragments j = 2 jp, 2 jp + 1 of this thread are one 16-B unit, at
+    // ((W * 16 + f / 2) * 64 + lane) of the slab for the float offset ((W * 32 + f) * 64 + lane) * 4
+    unsigned hoff[2];
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int u = off[2 * jp] >> 2;
+      hoff[jp] = (unsigned)((((u >> 7) << 6) + (u & 63)) * 16);
+    }
+    const char* hs = reinterpret_cast<const char*>(p.sk_slabs);
+    for (int bb = b0; bb <= b1; bb += 4) {  // 8 loads in flight (clamped, weighted as below)
+      u32x4 x[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const char* sl = hs + (size_t)(2 * ((bb + u <= b1 ? bb + u : b1) * p.sk_tiles + tile) + 1) * kTileElems * 4;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) x[u][jp] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sl + hoff[jp]));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float k = bb + u <= b1 ? 1.f : 0.f;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          union { u32x4 u; _Float16 h[8]; } pk;
+          pk.u = x[u][jp];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[2 * jp][r] += (float)pk.h[r] * k;
+            v[2 * jp + 1][r] += (float)pk.h[4 + r] * k;
+          }
+        }
+      }
+    }
+  } else
   // 4 slabs per round, all 16 loads issued before the adds (clamped indices: no conditional
   // load; a clamped duplicate is multiplied by 0)
   for (int bb = b0; bb <= b1; bb += 4) {
@@ -2061,17 +2113,8 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
     return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
   };
   const int wa = w >> 2, wb = w & 3;
-  {
-    const int u = threadIdx.x + 256 * kq, f = u >> 6, lane = u & 63;
-    const int off = ((w * 32 + f) * 64 + lane) * 4;
-    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int bb = b0; bb <= b1; bb += 4) {  // 4 slab loads in flight (clamped, weighted)
-      f32x4 x[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) x[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab(bb + q <= b1 ? bb + q : b1) + off));
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v += x[q] * (bb + q <= b1 ? 1.f : 0.f);
-    }
+  // one output fragment f of GEMM wave w for this lane, summed over the pieces (v)
+  auto emit = [&](int f, int lane, f32x4 v) {
     const int mi = f >> 2, ni = f & 3;
     const int rb = 128 * (mi >> 2) + 64 * wa + 16 * (mi & 3), cb = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
     // swapped orientation (as the dZ epilogue): out[m = rb + (lane & 15)][n = cb + 4 (lane >> 4) + r]
@@ -2116,6 +2159,48 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
       f32x4* o = reinterpret_cast<f32x4*>(p.out + row * p.ldo + col);
       *o = p.accum ? *o + v : v;
     }
+  };
+  if (pm && p.sk_half) {
+    // fp16 slabs (sk_fixup): one 16-B unit = fragments 2 q, 2 q + 1 of a lane; blocks kq < 4
+    // cover the wave's 16 x 64 units, one unit (two fragments) per thread
+    if (kq >= 4) return;
+    const int u = threadIdx.x + 256 * kq, q = u >> 6, lane = u & 63;
+    const size_t hoff = (size_t)((w * 16 + q) * 64 + lane) * 16;
+    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    for (int bb = b0; bb <= b1; bb += 4) {  // 4 slab loads in flight (clamped, weighted)
+      u32x4 x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        x[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+            reinterpret_cast<const char*>(slab(bb + k <= b1 ? bb + k : b1)) + hoff));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float wt = bb + k <= b1 ? 1.f : 0.f;
+        union { u32x4 u; _Float16 h[8]; } pk;
+        pk.u = x[k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] += (float)pk.h[r] * wt;
+          v1[r] += (float)pk.h[4 + r] * wt;
+        }
+      }
+    }
+    emit(2 * q, lane, v0);
+    emit(2 * q + 1, lane, v1);
+    return;
+  }
+  {
+    const int u = threadIdx.x + 256 * kq, f = u >> 6, lane = u & 63;
+    const int off = ((w * 32 + f) * 64 + lane) * 4;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int bb = b0; bb <= b1; bb += 4) {  // 4 slab loads in flight (clamped, weighted)
+      f32x4 x[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(slab(bb + q <= b1 ? bb + q : b1) + off));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v += x[q] * (bb + q <= b1 ? 1.f : 0.f);
+    }
+    emit(f, lane, v);
   }
 }
 

@@ -1102,6 +1102,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fwd_stream_enabled", &ntxent::fwd_stream_enabled);
   m.def("set_splitk_piece_major", &ntxent::set_splitk_piece_major, py::arg("on"));
   m.def("splitk_piece_major", &ntxent::splitk_piece_major);
+  m.def("set_splitk_half", &ntxent::set_splitk_half, py::arg("on"));
+  m.def("splitk_half", &ntxent::splitk_half);
+  m.def("set_splitk_dz_half", &ntxent::set_splitk_dz_half, py::arg("on"));
+  m.def("splitk_dz_half", &ntxent::splitk_dz_half);
   m.def("set_diag_upper", &ntxent::set_diag_upper, py::arg("on"));
   m.def("diag_upper_enabled", &ntxent::diag_upper_enabled);
   m.def("set_superblock_order", &ntxent::set_superblock_order, py::arg("on"));

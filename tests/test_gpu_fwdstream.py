@@ -77,7 +77,9 @@ def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
     from test_gpu_kernels import _oracle
 
     _, h = _inputs(rows, dim, torch.bfloat16, seed=41)
-    old = ext.splitk_piece_major()
+    old, old_half = ext.splitk_piece_major(), ext.splitk_half()
+    ext.set_splitk_half(False)  # fp32 slabs both ways (the fp16 slabs: test_splitk_half_slabs)
+    ext.set_splitk_dz_half(False)
     outs = {}
     try:
         for pm in (True, False):
@@ -89,6 +91,8 @@ def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
             outs[pm] = (loss.item(), g.float())
     finally:
         ext.set_splitk_piece_major(old)
+        ext.set_splitk_half(old_half)
+        ext.set_splitk_dz_half(True)
     (la, ga), (lb, gb) = outs[True], outs[False]
     assert abs(la - lb) <= 1e-5 * abs(lb)
     scale = gb.abs().max().item()
@@ -96,6 +100,45 @@ def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
     if compute != "fp8":
         lo, _ = _oracle(h, 0.07)
         assert abs(la - lo) <= 2e-4 * abs(lo)
+
+
+@pytest.mark.parametrize("rows,dim,compute", [(2048, 8192, "fp16"), (1024, 4096, "bf16"), (2048, 8192, "fp32"),
+                                              (2048, 4096, "fp8"), (8192, 512, "fp16"), (8192, 512, "bf16")])
+def test_splitk_half_slabs(ext, rows, dim, compute):
+    """Piece-major split-K forward and dZ with fp16 partial tiles (the default for 2-byte plans)
+    against fp32 slabs: each piece is rounded once to fp16 before the fp32 sum, so the kept cosines
+    and dZ move by a few fp16 ulps at most. fp32 and fp8 plans keep fp32 slabs (bitwise equal
+    either way). 8192 x 512 splits only the dZ."""
+    import ntxent_amd
+    from test_gpu_kernels import _oracle
+
+    assert ext.splitk_half(), "fp16 slabs are the default"
+    _, h = _inputs(rows, dim, torch.float32 if compute == "fp32" else torch.bfloat16, seed=43)
+    outs = {}
+    try:
+        for half in (True, False):
+            ext.set_splitk_half(half)
+            ext.set_splitk_dz_half(half)
+            x = h.clone().requires_grad_(True)
+            loss = ntxent_amd.ntxent_loss(x, 0.07, compute=compute)
+            (g,) = torch.autograd.grad(loss, x)
+            torch.cuda.synchronize()
+            outs[half] = (loss.item(), g.float())
+    finally:
+        ext.set_splitk_half(True)
+        ext.set_splitk_dz_half(True)
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    if compute in ("fp32", "fp8"):
+        assert la == lb and torch.equal(ga, gb), "fp32 / fp8 plans must not use fp16 slabs"
+        return
+    assert abs(la - lb) <= 1e-4 * abs(lb)
+    assert (ga - gb).abs().max().item() <= 1e-2 * gb.abs().max().item()
+    lo, go = _oracle(h, 0.07)
+    assert abs(la - lo) <= 2e-4 * abs(lo)
+    # the gradient error against the fp64 oracle stays within 25 % of the fp32-slab one
+    ea = (ga.double().cpu() - go).abs().max().item()
+    eb = (gb.double().cpu() - go).abs().max().item()
+    assert ea <= 1.25 * eb + 1e-6, (ea, eb)
 
 
 @pytest.mark.parametrize("rows,dim,compute,T", [
