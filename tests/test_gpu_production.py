@@ -184,12 +184,18 @@ def test_splitk_reduce_matches_stream_k(ext, rows, dim, T, compute):
     assert fwd >= 2 or dz >= 2
     dt = torch.float32 if compute == "fp32" else torch.bfloat16
     h = _views(rows, dim, seed=11 + dim, noise=2.0, dtype=dt)  # noisy views: O(1) loss
-    l0, g0 = _run(h, T, compute)
-    ext.set_splitk_reduce(False)
+    # reduce launch vs fixup on the same fp32 partials (the default fp16 slabs of 2-byte plans:
+    # test_gpu_fwdstream.py::test_splitk_half_slabs; the oracle check below runs the default)
+    ext.set_splitk_half(False)
+    ext.set_splitk_dz_half(False)
     try:
+        l0, g0 = _run(h, T, compute)
+        ext.set_splitk_reduce(False)
         l1, g1 = _run(h, T, compute)
     finally:
         ext.set_splitk_reduce(True)
+        ext.set_splitk_half(True)
+        ext.set_splitk_dz_half(True)
     assert abs(l1 - l0) <= 1e-6 * max(1.0, abs(l0)), (l0, l1)
     # summation order of the K pieces differs: a few output ulps (bf16 gradient)
     assert (g1.float() - g0.float()).abs().max().item() <= 1e-2 * g0.float().abs().max().item()
