@@ -258,7 +258,7 @@ bool splitk_piece_major();
 // on; off: fp32 slabs, twice the bytes written by the GEMM and read by sk_reduce_kernel)
 void set_splitk_half(bool on);
 bool splitk_half();
-// the same for the split-K dZ (sk_dz_reduce_kernel)
+// the same for the split-K dZ (sk_dz_reduce_kernel; default off)
 void set_splitk_dz_half(bool on);
 bool splitk_dz_half();
 // Diagonal remainder of the forward: upper 64x64 regions only, K halves for the off-diagonal ones

@@ -1086,7 +1086,8 @@ static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient 
 static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
 static std::atomic<bool> g_sk_piece_major{true};  // split-K forward: tile-aligned pieces, piece-major blocks
 static std::atomic<bool> g_sk_half{true};        // piece-major split-K forward of 2-byte plans: fp16 slabs
-static std::atomic<bool> g_sk_dz_half{true};     // piece-major split-K dZ of 2-byte plans: fp16 slabs
+static std::atomic<bool> g_sk_dz_half{false};    // piece-major split-K dZ of 2-byte plans: fp16 slabs
+                                                 // (opt-in: -3 us at config 2, moves dZ by ~2e-3 of max|g|)
 static std::atomic<bool> g_diag_up{true};        // diagonal remainder: upper regions only (diag_up_kernel)
 static std::atomic<bool> g_sb_order{true};       // own-block tile order in 8-panel superblocks (own_block_tiles)
 void set_diag_subtiles(bool on) { g_diag_sub = on; }

@@ -92,7 +92,7 @@ def test_splitk_piece_major_matches_tile_major(ext, rows, dim, compute):
     finally:
         ext.set_splitk_piece_major(old)
         ext.set_splitk_half(old_half)
-        ext.set_splitk_dz_half(True)
+        ext.set_splitk_dz_half(False)
     (la, ga), (lb, gb) = outs[True], outs[False]
     assert abs(la - lb) <= 1e-5 * abs(lb)
     scale = gb.abs().max().item()
@@ -112,7 +112,7 @@ def test_splitk_half_slabs(ext, rows, dim, compute):
     import ntxent_amd
     from test_gpu_kernels import _oracle
 
-    assert ext.splitk_half(), "fp16 slabs are the default"
+    assert ext.splitk_half() and not ext.splitk_dz_half(), "fp16 forward slabs are the default, dZ opt-in"
     _, h = _inputs(rows, dim, torch.float32 if compute == "fp32" else torch.bfloat16, seed=43)
     outs = {}
     try:
@@ -126,7 +126,7 @@ def test_splitk_half_slabs(ext, rows, dim, compute):
             outs[half] = (loss.item(), g.float())
     finally:
         ext.set_splitk_half(True)
-        ext.set_splitk_dz_half(True)
+        ext.set_splitk_dz_half(False)
     (la, ga), (lb, gb) = outs[True], outs[False]
     if compute in ("fp32", "fp8"):
         assert la == lb and torch.equal(ga, gb), "fp32 / fp8 plans must not use fp16 slabs"

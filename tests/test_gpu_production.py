@@ -186,6 +186,7 @@ def test_splitk_reduce_matches_stream_k(ext, rows, dim, T, compute):
     h = _views(rows, dim, seed=11 + dim, noise=2.0, dtype=dt)  # noisy views: O(1) loss
     # reduce launch vs fixup on the same fp32 partials (the default fp16 slabs of 2-byte plans:
     # test_gpu_fwdstream.py::test_splitk_half_slabs; the oracle check below runs the default)
+    old_dz = ext.splitk_dz_half()
     ext.set_splitk_half(False)
     ext.set_splitk_dz_half(False)
     try:
@@ -195,7 +196,7 @@ def test_splitk_reduce_matches_stream_k(ext, rows, dim, T, compute):
     finally:
         ext.set_splitk_reduce(True)
         ext.set_splitk_half(True)
-        ext.set_splitk_dz_half(True)
+        ext.set_splitk_dz_half(old_dz)
     assert abs(l1 - l0) <= 1e-6 * max(1.0, abs(l0)), (l0, l1)
     # summation order of the K pieces differs: a few output ulps (bf16 gradient)
     assert (g1.float() - g0.float()).abs().max().item() <= 1e-2 * g0.float().abs().max().item()
