@@ -393,21 +393,7 @@ int main(int argc, char** argv) {
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
     else if (a == "--no-small") o.small = false;
-    else if (a == "--no-strips") ntxent::set_diag_strips(false);
-    else if (a == "--no-splitk") ntxent::set_splitk_reduce(false);
-    else if (a == "--no-subtiles") ntxent::set_diag_subtiles(false);
-    else if (a == "--no-coef-perm") ntxent::set_coef_lane_permute(false);
-    else if (a == "--no-dzsym") ntxent::set_dz_sym(false);
-    else if (a == "--dzsym") ntxent::set_dz_sym(true);
-    else if (a == "--fwd-stream") ntxent::set_fwd_stream(true);
-    else if (a == "--no-normfuse") ntxent::set_norm_fuse(false);
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
-    else if (a == "--no-fwd-stream") ntxent::set_fwd_stream(false);
-    else if (a == "--no-sk-pm") ntxent::set_splitk_piece_major(false);
-    else if (a == "--no-sk-half") ntxent::set_splitk_half(false);
-    else if (a == "--no-sk-dz-half") ntxent::set_splitk_dz_half(false);
-    else if (a == "--no-diag-up") ntxent::set_diag_upper(false);
-    else if (a == "--zorder") ntxent::set_superblock_order(false);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "--negatives") {
@@ -430,17 +416,8 @@ int main(int argc, char** argv) {
                   "  --gpus N --proc-rank r --uid-file F [--shared-gpu]: rank r of N processes over RCCL\n"
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
-                  "  --no-splitk: tile-starved forward by the stream-K fixup instead of split-K + reduce (A/B)\n"
-                  "  --no-strips: forward remainder tiles by the stream-K split instead of diagonal strips (A/B)\n"
-                  "  --dzsym / --no-dzsym: backward from the upper-triangular C + Zq (launch_dz_sym), or through\n"
-                  "              mirrored coefficient tiles + ZqT + launch_dz (default)\n"
-                  "  --no-fwd-stream: forward GEMM drains after each item and issues the next item's prologue\n"
-                  "              after its epilogue (A/B; default: the operand streams run into the next item)\n"
-                  "  --no-sk-pm: split-K forward with the tile-major straddling pieces (A/B; default piece-major)\n"
-                  "  --no-sk-half: fp32 split-K forward slabs (A/B; default fp16 for 2-byte plans)\n"
-                  "  --no-sk-dz-half: fp32 split-K dZ slabs (A/B; default fp16 for 2-byte plans)\n"
-                  "  --no-diag-up: diagonal remainder over all 16 sub-tiles (A/B; default: upper regions only)\n"
-                  "  --zorder: own-block tiles in Z-order (A/B; default: 8-panel superblocks)\n");
+                  "  (the measured A/B alternatives of earlier rounds are deleted; build-time variants:\n"
+                  "   tools/build_variant.sh)\n");
       return 0;
     }
   }

@@ -50,9 +50,6 @@ struct EngineConfig {
   DType compute = DType::F16;
 #endif
   bool keep_cos = true;       // keep cosine tiles for the backward (else recompute them)
-  // dZ from the upper-triangular coefficient tiles and the gathered Zq rows (launch_dz_sym) on
-  // eligible plans: no mirrored C tiles, no ZqT transpose / gather
-  bool dz_sym = true;
   // FP8 compute: the backward's coefficient matrix and Z^T in e4m3 too (Q8Stats; world 1).
   // -1: the process default (set_fp8_backward), 0 / 1: off / on.
   int fp8_backward = -1;
@@ -112,7 +109,6 @@ class Engine {
   int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
-  bool sym_ = false;           // launch_dz_sym backward (EngineConfig::dz_sym)
   bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
   float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
   float* dot_ = nullptr;       // dot [Rpad]
@@ -135,7 +131,8 @@ class Engine {
   void backward_sym(const float* grad_out, void* dh, hipStream_t s);
   const int4* dz_rows(int m0, int m1) const;
   void dz_view(const char* abuf, long a_tile0, long a_panel_tiles, const char* bbuf, int b_block0, long b_col0,
-               int k_tiles, int m0, int m1, void* out, bool accum, bool out_f16, hipStream_t s);
+               int k_tiles, int m0, int m1, void* out, bool accum, bool out_f16, hipStream_t s,
+               const GemmWorkspace& ws);
   bool q8_ = false;            // fp8 backward (e4m3 C and Z^T, EngineConfig::fp8_backward)
   float* q8_mneg_ = nullptr;   // Q8Stats: negatives-only row max [Rpad], min LSE [1]
   float* q8_lmin_ = nullptr;

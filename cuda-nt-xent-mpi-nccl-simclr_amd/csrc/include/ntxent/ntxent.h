@@ -14,8 +14,8 @@
 //     tiles are computed; each produces row AND column partials;
 //   * the backward is rank-local: C = P + P^T - 2*I_pos is formed from the stored
 //     cosines + all-gathered LSE (no atomics, deterministic), then dZ = C * Z runs on
-//     MFMA; a fused row kernel applies grad_out/(2N*tau) and the L2-normalisation
-//     backward.
+//     MFMA; the dZ GEMM's epilogue applies grad_out/(2N*tau) and the L2-normalisation
+//     backward (dh = c1 g - c2 h, with dot_i = z_i . g_i from the coefficient pass).
 //
 // Layout conventions (see Geometry):
 //   * R local rows = [view1 (n rows); view2 (n rows)], positive p(i) = (i + n) mod R.
@@ -148,10 +148,10 @@ struct GemmWorkspace {
   void* ptr = nullptr;
   size_t bytes = 0;
   int num_cus = 256;    // sizes the counter region and the slabs (the device's CU count)
-  // Grid cap of the persistent schedule (0: num_cus). A GEMM launched while an RCCL transfer is
-  // in flight leaves num_cus - sched_cus CUs free for the communication kernels: the persistent
-  // blocks (128 KiB LDS, the whole register file) would otherwise hold every CU until the GEMM
-  // ends and the "overlapped" transfer would start only then.
+  // Grid cap of the persistent schedule (0: num_cus), set per launch. A GEMM launched while an
+  // RCCL transfer is in flight leaves num_cus - sched_cus CUs free for the communication kernels:
+  // the persistent blocks (128 KiB LDS, the whole register file) would otherwise hold every CU
+  // until the GEMM ends and the "overlapped" transfer would start only then.
   int sched_cus = 0;
 };
 size_t gemm_workspace_bytes(int ntiles, int num_cus);
@@ -192,41 +192,25 @@ struct BlockView {
 // i.e. rank q's part slots [rank*row_tiles + mt] for its rows.
 // diag_tail: the last `diag_tail` entries of `tiles` are kTileDiag tiles (own_diag_tail(g) for
 // a launch that ends with the own block, else 0). When the persistent GEMM's tile count leaves a
-// remainder of at most that many tiles after its whole rounds, the remainder runs as 16-row
-// strips in a second, short launch (diag_strip_kernel) instead of a third round or a stream-K
-// split (528 forward tiles at B = 4096/view: 2 rounds + strips instead of ~2.9 rounds).
+// remainder of at most that many tiles after its whole rounds, the remainder runs as upper 64x64
+// regions in a second, short launch (diag_up_kernel) instead of a third round or a stream-K
+// split (528 forward tiles at B = 4096/view: 2 rounds + 16 diagonal tiles instead of ~2.9 rounds).
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
                       const BlockView& bv = BlockView{}, float2* part_x = nullptr,
                       int diag_tail = 0, hipEvent_t main_done = nullptr);
-// main_done (optional): recorded on `stream` right after the persistent GEMM, before the strips.
-// Strip finishing of the forward's remainder (on by default; off = the stream-K split, for A/B).
-void set_diag_strips(bool on);
-// Diagonal remainder as 64x64 sub-tiles (default) or 16-row strips (off, for A/B).
-void set_diag_subtiles(bool on);
-bool diag_strips_enabled();
-// Split-K forward for own-block launches with fewer tiles than CUs and long K (on by default;
-// off = the stream-K schedule's serial last-arriver fixup, for A/B): K pieces of every tile
-// publish fp32 partial slabs and a second launch sums them and runs the epilogue in strips.
-// Coefficient pass row-major stores from lane-permuted registers (one row per 4-lane quad; on by
-// default, off for A/B).
-void set_coef_lane_permute(bool on);
-bool coef_lane_permute();
-void set_splitk_reduce(bool on);
-bool splitk_reduce_enabled();
+// main_done (optional): recorded on `stream` right after the persistent GEMM, before the remainder.
+// Split-K for own-block launches with fewer tiles than CUs and long K (BASELINE config 4): K
+// pieces of every tile publish partial slabs and a second launch sums them and runs the
+// epilogue in strips; fwd_splitk_pieces = pieces per tile (0: the stream-K schedule).
+int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
 // Small-problem path (on by default; off = the large-problem pipeline for every shape) and its
-// backward column splits (0 = small_bwd_splits).
+// backward column splits (0 = small_bwd_splits). Test hooks: process-wide.
 void set_small_path(bool on);
 bool small_path_enabled();
 void set_small_splits(int n);
 int small_splits_override();
-// CUs the similarity GEMMs launched while it is non-zero leave free for communication kernels
-// (the data-parallel paths set it around launches that overlap an RCCL transfer); returns the
-// old value.
-int set_grid_reserve(int n);
-int grid_reserve();
-int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
 
 // Merge the negatives-only partials per positive pair -> lse2 = logaddexp2(lse_neg, ypos)
 // into lse2_all[rank*Rpad + i] and the positive coefficient cpos[i] = C_i,p(i) =
@@ -245,29 +229,7 @@ int lse_scratch_floats(const Geometry& g);
 // epilogue), Z^T by 256. Q8Stats carries the LSE pass's extra outputs: mneg2 [Rpad] (each row's
 // negatives-only max logit, log2 units), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
 // bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
-void set_fp8_backward(bool on);  // default: see ntxent_kernels.hip
-// Forward GEMM: the operand streams run from one whole-tile work item into the next, so the next
-// item's first K-steps load under the epilogue (default on; off for A/B)
-void set_fwd_stream(bool on);
-bool fwd_stream_enabled();
-// Split-K forward (tile-starved shapes): tile-aligned K pieces assigned piece-major to the blocks
-// (default on; off: the flattened tile-major split with straddling pieces, for A/B)
-void set_splitk_piece_major(bool on);
-bool splitk_piece_major();
-// piece-major split-K forward of fp16/bf16 plans: pieces publish fp16 partial tiles (default
-// on; off: fp32 slabs, twice the bytes written by the GEMM and read by sk_reduce_kernel)
-void set_splitk_half(bool on);
-bool splitk_half();
-// the same for the split-K dZ (sk_dz_reduce_kernel; default off)
-void set_splitk_dz_half(bool on);
-bool splitk_dz_half();
-// Diagonal remainder of the forward: upper 64x64 regions only, K halves for the off-diagonal ones
-// (diag_up_kernel; default on; off: all 16 regions over the whole K, diag_sub_kernel)
-void set_diag_upper(bool on);
-bool diag_upper_enabled();
-// Own-block tile order (plans built afterwards): 8-panel superblocks (default) or Z-order (A/B)
-void set_superblock_order(bool on);
-bool superblock_order_enabled();
+void set_fp8_backward(bool on);  // default off (opt-in: 5e-2 of max|g| gradient error)
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
 int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad
@@ -289,8 +251,6 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 // tiles with slot = (q - rank - 1) mod W (partners rank+1, rank+2, ... in order): tile (mt, nt)
 // lands transposed at mbuf tile (slot, nt % row_tiles, mt), i.e. the block C_{q,rank} that
 // multiplies this rank's rows in rank q's gradient; consecutive slots stack into one tall A.
-// upper_only: write only the tiles of `tiles` themselves (no mirrored lower own-block tiles): the
-// layout launch_dz_sym reads.
 // dotp (optional, [dot_slots(g)][Rpad] floats, slot-major): partials of dot_i = sum_j C_ij cos_ij, the
 // z_i . g_i of the normalisation backward, for the fused dZ epilogue (NormFuse); every slot is
 // written (all-gather layout, own-block tiles + remote tiles of the plan).
@@ -300,8 +260,7 @@ int dot_slots(const Geometry& g);
 // the partials of the dequantised coefficients (plus the exact positive term).
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf = nullptr, bool upper_only = false, float* dotp = nullptr,
-                 const Q8Stats* q8 = nullptr);
+                 void* mbuf = nullptr, float* dotp = nullptr, const Q8Stats* q8 = nullptr);
 // dot[Rpad] = row sums of dotp.
 void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream);
 
@@ -317,10 +276,8 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 // the normalisation backward's read; |dZ| <= ~4, fp16 keeps 11 bits against the bf16/fp16 dh).
 // Fused normalisation backward of the dZ GEMM's epilogue: dh = grad_out/(2N tau) inv (g - z dot)
 // computed per tile from the fp16-staged g, h, inv and dot (launch_dot_reduce); the dZ slab is
-// not written. The launchers return whether they fused (not for split-K dZ pieces or d % 8 != 0:
-// then the slab is written and launch_norm_bwd runs as before).
-void set_norm_fuse(bool on);  // default on; off = dZ slab + launch_norm_bwd (A/B)
-bool norm_fuse_enabled();
+// not written. The launchers return whether they fused (not for fp32 plans or d % 8 != 0: then
+// the slab is written and launch_norm_bwd runs).
 struct NormFuse {
   const void* h = nullptr;
   DType in = DType::BF16;
@@ -335,16 +292,8 @@ bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* ti
                void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false,
                const NormFuse* nf = nullptr, const Q8Stats* q8 = nullptr, const float* cpos = nullptr);
 
-// dZ = C * Zq (all-gather layout) from the coefficient tiles launch_coef(..., upper_only) wrote
-// (own-block upper triangle + remote tiles; a lower own tile is read as the transpose of the
-// stored one) and the normalised rows zq_all [W * Rpad][ld_k] themselves (no ZqT): 64 MiB less
-// coefficient store and no transpose at the headline. Plans: dz_sym_eligible.
-bool dz_sym_eligible(const Geometry& g, DType comp);
-void set_dz_sym(bool on);  // default on; off = coefficient mirrors + ZqT + launch_dz (A/B)
-bool dz_sym_enabled();
-bool launch_dz_sym(DType comp, const void* cbuf, const void* zq_all, const int4* tiles, int ntiles, void* dz,
-                   const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = true,
-                   const NormFuse* nf = nullptr);
+// (A dZ that reads only the upper-triangular C, mirrored K-steps and Z through transposed LDS reads,
+// measured 33 us slower than the mirrored C + Z^T path at the headline: profiles/r3/dzexp.)
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first

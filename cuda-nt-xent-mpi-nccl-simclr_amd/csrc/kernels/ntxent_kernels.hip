@@ -15,7 +15,6 @@
 #include "../include/ntxent/ntxent.h"
 #include "device_common.h"
 #include "sim_gemm.h"
-#include "dz_sym.h"
 
 #include <atomic>
 #include <algorithm>
@@ -743,7 +742,6 @@ void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
 
 dev::SimParams base_params(const Geometry& g) {
   dev::SimParams p{};
-  p.fwd_stream = fwd_stream_enabled() ? 1 : 0;
   p.R = g.rows;
   p.Rpad = g.rows_pad;
   p.n_half = g.rows / 2;
@@ -849,7 +847,7 @@ static void zorder(std::vector<int4>& t, size_t first, size_t last) {
 static std::vector<int4> own_block_tiles(const Geometry& g) {
   std::vector<int4> tiles;
   const int own = g.rank * g.row_tiles, rt = g.row_tiles;
-  if (rt % 8 == 0 && rt >= 16 && superblock_order_enabled()) {
+  if (rt % 8 == 0 && rt >= 16) {
     const int nb = rt / 8;
     for (int a = 0; a < nb; ++a)
       for (int b = a + 1; b < nb; ++b)
@@ -1069,68 +1067,31 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 
-// ---- runtime switches: every process-wide toggle of the library lives here (atomics; the
-//      defaults are the measured-fastest choices, the setters exist for A/B tests) ----------
-static std::atomic<bool> g_diag_sub{true};       // diagonal remainder as 64x64 sub-tiles (else strips)
-static std::atomic<bool> g_diag_strips{true};    // forward remainder after whole rounds as strips/sub-tiles
-static std::atomic<bool> g_coef_perm{true};      // coefficient pass: lane-permuted row-major stores
-static std::atomic<bool> g_splitk_reduce{true};  // split-K forward / dZ for tile-starved launches
+// ---- runtime switches: every process-wide toggle of the library lives here (atomics). Only
+//      behaviour switches remain: the small-problem path (off = the large-problem pipeline at
+//      every shape, so tests can exercise it on small inputs), its two test overrides, and the
+//      opt-in fp8 backward. Measured A/B losers are deleted, not kept behind toggles; the CUs a
+//      GEMM leaves free for communication are a per-launch argument (GemmWorkspace::sched_cus).
 static std::atomic<bool> g_small_path{true};     // one-launch small-problem forward / backward
 static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
 static std::atomic<int> g_small_fuse_rows{-1};   // small forward: fused row prologue up to R rows (-1: default)
-static std::atomic<int> g_grid_reserve{0};       // CUs the GEMMs leave free for overlapped RCCL kernels
-static std::atomic<bool> g_dz_sym{false};        // dZ from the upper-triangular C and Zq (launch_dz_sym): A/B
-                                                 // (profiles/r3/ab: its GEMM is slower than coef mirrors + ZqT save)
-static std::atomic<bool> g_norm_fuse{true};      // normalisation backward in the dZ epilogue (NormFuse)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
-static std::atomic<bool> g_fwd_stream{true};     // forward GEMM: operand streams continue into the next item
-static std::atomic<bool> g_sk_piece_major{true};  // split-K forward: tile-aligned pieces, piece-major blocks
-static std::atomic<bool> g_sk_half{true};        // piece-major split-K forward of 2-byte plans: fp16 slabs
-static std::atomic<bool> g_sk_dz_half{false};    // piece-major split-K dZ of 2-byte plans: fp16 slabs
-                                                 // (opt-in: -3 us at config 2, moves dZ by ~2e-3 of max|g|)
-static std::atomic<bool> g_diag_up{true};        // diagonal remainder: upper regions only (diag_up_kernel)
-static std::atomic<bool> g_sb_order{true};       // own-block tile order in 8-panel superblocks (own_block_tiles)
-void set_diag_subtiles(bool on) { g_diag_sub = on; }
-void set_diag_strips(bool on) { g_diag_strips = on; }
-bool diag_strips_enabled() { return g_diag_strips.load(); }
-void set_coef_lane_permute(bool on) { g_coef_perm = on; }
-bool coef_lane_permute() { return g_coef_perm.load(); }
-void set_splitk_reduce(bool on) { g_splitk_reduce = on; }
-bool splitk_reduce_enabled() { return g_splitk_reduce.load(); }
 void set_small_path(bool on) { g_small_path = on; }
 bool small_path_enabled() { return g_small_path.load(); }
 void set_small_splits(int n) { g_small_splits = std::max(0, n); }
 int small_splits_override() { return g_small_splits.load(); }
 void set_small_fuse_rows(int rows) { g_small_fuse_rows = rows < 0 ? -1 : rows; }
 int small_fuse_rows_override() { return g_small_fuse_rows.load(); }
-int set_grid_reserve(int n) { return g_grid_reserve.exchange(std::max(0, n)); }
-int grid_reserve() { return g_grid_reserve.load(); }
-void set_dz_sym(bool on) { g_dz_sym = on; }
-bool dz_sym_enabled() { return g_dz_sym.load(); }
-void set_fwd_stream(bool on) { g_fwd_stream = on; }
-void set_splitk_piece_major(bool on) { g_sk_piece_major = on; }
-void set_splitk_half(bool on) { g_sk_half = on; }
-bool splitk_half() { return g_sk_half.load(); }
-void set_splitk_dz_half(bool on) { g_sk_dz_half = on; }
-bool splitk_dz_half() { return g_sk_dz_half.load(); }
-void set_diag_upper(bool on) { g_diag_up = on; }
-void set_superblock_order(bool on) { g_sb_order = on; }
-bool superblock_order_enabled() { return g_sb_order.load(); }
-bool diag_upper_enabled() { return g_diag_up.load(); }
-bool splitk_piece_major() { return g_sk_piece_major.load(); }
-bool fwd_stream_enabled() { return g_fwd_stream.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
 int q8_ldt(const Geometry& g) { return g.rows_pad; }
-void set_norm_fuse(bool on) { g_norm_fuse = on; }
-bool norm_fuse_enabled() { return g_norm_fuse.load(); }
 
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
 // partial slabs serially (BASELINE config 4: 36 tiles x 128 K-steps, fixup ~40 % of the GEMM).
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
-  if (!splitk_reduce_enabled() || diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
+  if (diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
   const int pcs = std::min(cus / ntiles, nk / 8);
   return pcs >= 2 ? pcs : 0;
 }
@@ -1154,20 +1115,29 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.sc = static_cast<char*>(sc);
   p.b_tile0 = bv.b_tile0;
   p.part_x = part_x;
-  // Whole rounds on the persistent GEMM; a remainder that fits in the diagonal tail runs as
-  // strips (diag_strip_kernel) after it instead of as a third round / stream-K split. fp8
-  // launches keep the stream-K schedule.
-  int nstrip = 0;
   const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
-  if (diag_tail > 0 && comp != DType::FP8 && diag_strips_enabled()) {
+  const int nk_tile = (int)(kb / kKStepBytes);
+  // Whole rounds on the persistent GEMM. A remainder of diagonal tiles (the own block's tail)
+  // runs after them as upper 64x64 regions (diag_up_kernel: 10 of a tile's 16 regions, the
+  // coefficient pass mirrors the rest) instead of a third round / stream-K split: 528 forward
+  // tiles at B = 4096/view are 2 rounds + 16 diagonal tiles. fp8 launches and short K (< 4
+  // K-steps: no K halves) keep the stream-K split of the remainder.
+  int nstrip = 0;
+  if (diag_tail > 0 && !f8 && nk_tile >= 4) {
     const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
-    if (q >= 1 && rem > 0 && rem <= diag_tail) nstrip = rem;
+    // 10 arrival tickets per tile in the counter region, 12 half-region fp32 partials per tile
+    // in the slab region
+    if (q >= 1 && rem > 0 && rem <= diag_tail && 10 * rem <= 2 * ws.num_cus &&
+        (size_t)12 * rem * 4096 <= (size_t)2 * ws.num_cus * kTileElems)
+      nstrip = rem;
   }
   const int nmain = ntiles - nstrip;
-  const int nk_tile = (int)(kb / kKStepBytes);
   const int pieces = part_x == nullptr ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
   int grid;
-  if (pieces > 0) {  // split-K: every piece publishes its slab, sk_reduce_kernel finishes the tiles
+  if (pieces > 0) {
+    // split-K: tile-aligned pieces, piece-major over the blocks (the XCD-contiguous block runs
+    // then stream one K range of every row panel together: L2 reuse across the tiles,
+    // profiles/r3/splitk_pm); every piece publishes its slab, sk_reduce_kernel finishes the tiles
     NTXENT_CHECK(kb % kKStepBytes == 0, "K not aligned to the K step");
     p.nk = nk_tile;
     p.dp_tiles = 0;
@@ -1175,19 +1145,11 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
     p.ipb = (nk_tile + pieces - 1) / pieces;
     p.sk_cnt = static_cast<int*>(ws.ptr);
     p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-    if (splitk_piece_major()) {
-      // tile-aligned pieces, piece-major over the blocks: the XCD-contiguous block runs then
-      // stream one K range of every row panel together (L2 reuse across the tiles) instead of
-      // every K range of a few tiles (profiles/r3/splitk_pm)
-      p.sk_out = 2;
-      grid = (int)((nk_tile + p.ipb - 1) / p.ipb) * ntiles;
-      // fp16 partial tiles for 2-byte plans: the pieces are normalised-row dot products over a
-      // K range (|x| <= 1), summed in fp32 by the reduce; the kept cosines are 2-byte anyway
-      p.sk_half = (comp == DType::F16 || comp == DType::BF16) && g_sk_half.load() ? 1 : 0;
-    } else {
-      p.sk_out = 1;
-      grid = (int)(((long long)ntiles * nk_tile + p.ipb - 1) / p.ipb);
-    }
+    p.splitk = 1;
+    grid = (int)((nk_tile + p.ipb - 1) / p.ipb) * ntiles;
+    // fp16 partial tiles for 2-byte plans: the pieces are normalised-row dot products over a K
+    // range (|x| <= 1), summed in fp32 by the reduce; the kept cosines are 2-byte anyway
+    p.sk_half = (comp == DType::F16 || comp == DType::BF16) ? 1 : 0;
     NTXENT_CHECK(grid <= ws.num_cus && ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
                  "split-K forward: workspace too small");
   } else {
@@ -1206,42 +1168,18 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
     if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
       if (nstrip > 0) {
-        NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diag strips: row-major operands only");
+        NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diagonal remainder: row-major operands only");
         dev::SimParams q = p;
         q.tiles = tiles + nmain;
         if (q.sc) q.sc += (size_t)nmain * kTileElems * sizeof(typename dev::StoreT<Tc>::type);
+        q.sk_cnt = static_cast<int*>(ws.ptr);
+        q.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+        // row-group partials in the column-partial area of the workspace
+        float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
+                                                    (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
         const dim3 sg(nstrip * 16);
-        const bool one_wave = nstrip * 16 <= ws.num_cus;  // 3-stage ring, else 2 blocks per CU
-        // 64x64 sub-tiles (row-group tickets) unless K is short and the strips fit in one wave of
-        // blocks (config 2, d = 512: strips 7.4 vs sub-tiles 8.0 us; headline 17.0 vs 15.3,
-        // config 5 18.5 vs 12.9: profiles/r2/subtiles)
-        const bool sub = (p.kbytes / kKStepBytes) >= 16 || !one_wave;
-        const int nk_d = (int)(p.kbytes / kKStepBytes);
-        if (g_diag_sub.load() && sub && 4 * nstrip <= 2 * ws.num_cus) {
-          q.sk_cnt = static_cast<int*>(ws.ptr);
-          float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
-                                                      (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
-          // upper regions only (the coefficient pass mirrors a diagonal tile's regions), K halves
-          // for the off-diagonal ones: 10 tickets per tile, pair partials in the (idle) slab area.
-          // Measured (profiles/r3/diag_up): 14.4 vs 15.1 us at the headline (16 tiles, one block
-          // per CU), 13.7 vs 13.1 us at config 5 (32 tiles, two per CU): used for one wave only
-          if (g_diag_up.load() && nk_d >= 4 && one_wave && 10 * nstrip <= 2 * ws.num_cus &&
-              (size_t)12 * nstrip * 4096 <= (size_t)2 * ws.num_cus * kTileElems) {
-            q.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
-            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
-          } else if (p.fixed_shift) {
-            hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
-          } else {
-            hipLaunchKernelGGL((dev::diag_sub_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
-          }
-        } else if (p.fixed_shift) {
-          if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 3>), sg, dim3(256), 0, stream, q);
-          else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q);
-        } else {
-          if (one_wave) hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 0, 3>), sg, dim3(256), 0, stream, q);
-          else hipLaunchKernelGGL((dev::diag_strip_kernel<Tc, 0, 2>), sg, dim3(256), 0, stream, q);
-        }
+        if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
+        else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
       }
     }
   });
@@ -1312,10 +1250,9 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf, bool upper_only, float* dotp, const Q8Stats* q8) {
+                 void* mbuf, float* dotp, const Q8Stats* q8) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
-  p.no_mirror = upper_only ? 1 : 0;
   p.dotp = dotp;
   p.tiles = tiles;
   p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
@@ -1324,18 +1261,17 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
   p.lse2 = lse2_all;
   p.cpos = cpos;
   if (q8) {
-    NTXENT_CHECK(comp == DType::F16 && mbuf == nullptr && !upper_only && g.world == 1,
+    NTXENT_CHECK(comp == DType::F16 && mbuf == nullptr && g.world == 1,
                  "coef (fp8 backward): fp16 kept cosines, world 1, mirrored layout");
     p.q8_mneg = q8->mneg2;
     p.q8_lmin = q8->lmin;
-    hipLaunchKernelGGL((dev::coef_kernel<_Float16, true, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
+    hipLaunchKernelGGL((dev::coef_kernel<_Float16, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
     NTXENT_HIP_CHECK(hipGetLastError());
     return;
   }
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    if (coef_lane_permute()) hipLaunchKernelGGL((dev::coef_kernel<Tc, true>), dim3(16 * ntiles), dim3(64), 0, stream, p);
-    else hipLaunchKernelGGL((dev::coef_kernel<Tc, false>), dim3(16 * ntiles), dim3(64), 0, stream, p);
+    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(16 * ntiles), dim3(64), 0, stream, p);
   });
   NTXENT_HIP_CHECK(hipGetLastError());
 }
@@ -1416,16 +1352,10 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     p.ipb = (nk + pieces - 1) / pieces;
     p.sk_cnt = static_cast<int*>(ws.ptr);
     p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-    if (splitk_piece_major()) {  // as the forward's: an XCD streams one K range of every panel
-      p.sk_out = 2;
-      grid = (int)((nk + p.ipb - 1) / p.ipb) * ntiles;
-      // fp16 partial tiles for 2-byte plans (summed in fp32 by sk_dz_reduce_kernel, whose output
-      // is rounded to fp16 / the input dtype anyway)
-      p.sk_half = (comp == DType::F16 || comp == DType::BF16) && g_sk_dz_half.load() ? 1 : 0;
-    } else {
-      p.sk_out = 1;
-      grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
-    }
+    // piece-major, as the forward's: an XCD streams one K range of every panel. fp32 slabs (fp16
+    // ones measured -3 us at config 2 but moved dZ by ~2e-3 of max|g|: profiles/r3/skhalf)
+    p.splitk = 1;
+    grid = (int)((nk + p.ipb - 1) / p.ipb) * ntiles;
     NTXENT_CHECK(p.kbytes % kKStepBytes == 0 && grid <= ws.num_cus && ws.ptr != nullptr &&
                      ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
                  "split-K dZ: workspace too small");
@@ -1437,58 +1367,6 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
   });
-  if (pieces > 0) hipLaunchKernelGGL(dev::sk_dz_reduce_kernel, dim3(ntiles * 64), dim3(256), 0, stream, p);
-  NTXENT_HIP_CHECK(hipGetLastError());
-  return fused;
-}
-
-bool dz_sym_eligible(const Geometry& g, DType comp) {
-  // 16-bit operands (transposed LDS reads) and Zq rows that hold every column of a d-tile
-  // (dim_k == dim_n: the B half-tiles never read past a row)
-  return (comp == DType::F16 || comp == DType::BF16 || comp == DType::FP8) && g.dim_k == g.dim_n;
-}
-
-bool launch_dz_sym(DType comp, const void* cbuf, const void* zq_all, const int4* tiles, int ntiles, void* slabs,
-                   const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16, const NormFuse* nf) {
-  if (ntiles == 0) return false;
-  const DType bc = backward_dtype(comp);
-  NTXENT_CHECK(dz_sym_eligible(g, comp), "dz_sym: plan not eligible (16-bit backward dtype, dim_k == dim_n)");
-  const long long cs = 2;
-  dev::SimParams p = base_params(g);
-  p.A.base = static_cast<const char*>(cbuf);  // tiles [row_tiles][col_tiles], upper own block stored
-  if (std::getenv("NTXENT_DZSYM_NOMIR")) p.row_tile0 = 1 << 20;  // DIAGNOSTIC: full C, no mirrored steps
-  p.B.base = static_cast<const char*>(zq_all);
-  p.B.ld = (long long)g.ld_k * cs;
-  p.tiles = tiles;
-  p.kbytes = (long long)g.world * g.rows_pad * cs;
-  p.out = static_cast<float*>(slabs);
-  p.out_f16 = out_f16 ? 1 : 0;
-  p.ldo = g.dim_n;
-  p.slab_stride = (long long)g.rows_pad * g.dim_n;
-  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
-  const int nk = (int)(p.kbytes / kKStepBytes);
-  int pieces = fwd_splitk_pieces(ntiles, nk, cus, 1);
-  if (pieces < 3) pieces = 0;
-  int grid;
-  if (pieces > 0) {
-    p.nk = nk;
-    p.dp_tiles = 0;
-    p.sk_tiles = ntiles;
-    p.ipb = (nk + pieces - 1) / pieces;
-    p.sk_out = 1;
-    p.sk_cnt = static_cast<int*>(ws.ptr);
-    p.sk_slabs = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-    grid = (int)(((long long)ntiles * nk + p.ipb - 1) / p.ipb);
-    NTXENT_CHECK(grid <= ws.num_cus && ws.ptr != nullptr && ws.bytes >= gemm_workspace_bytes(ntiles, ws.num_cus),
-                 "split-K dZ: workspace too small");
-  } else {
-    grid = apply_schedule(p, ntiles, ws, stream);
-  }
-  const bool fused = apply_norm_fuse(p, nf, g);
-  if (bc == DType::BF16)
-    hipLaunchKernelGGL((dev::dz_sym_kernel<__bf16>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
-  else
-    hipLaunchKernelGGL((dev::dz_sym_kernel<_Float16>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
   if (pieces > 0) hipLaunchKernelGGL(dev::sk_dz_reduce_kernel, dim3(ntiles * 64), dim3(256), 0, stream, p);
   NTXENT_HIP_CHECK(hipGetLastError());
   return fused;

@@ -78,9 +78,6 @@ struct SimParams {
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
-  int fwd_stream;        // forward: operand streams run into the next whole-tile item (sim_gemm_kernel)
-  int no_mirror;         // coefficient pass: write only the stored (upper) own-block tiles (dz_sym_kernel
-                         // reads the lower ones transposed)
   // Fused normalisation backward (see dot_slots / dz_store):
   float* dotp;           // coefficient pass: partials of dot_i = sum_j C_ij cos_ij, [4 col_tiles][Rpad]
   const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
@@ -103,11 +100,11 @@ struct SimParams {
   long long ipb;         // stream-K K-steps per block
   float* sk_slabs;       // [2 * gridDim][256*256] fp32 partial tiles
   int* sk_cnt;           // [sk_tiles] arrival counters (zero at launch; self-cleaning)
-  int sk_out;            // forward split-K: every piece only publishes its slab; sk_reduce_kernel
-                         // (2: tile-aligned pieces of ipb K-steps, piece-major: block b = piece
-                         // (b / sk_tiles) of tile (b % sk_tiles), slab slot 2 b + 1)
-                         // sums a tile's slabs and runs its epilogue in row / column strips
-  int sk_half;           // piece-major split-K (sk_out == 2) of a 2-byte plan: fp16 partial tiles,
+  int splitk;            // split-K for tile-starved launches: tile-aligned pieces of ipb K-steps,
+                         // piece-major (block b = piece b / sk_tiles of tile b % sk_tiles, slab
+                         // slot 2 b + 1); every piece only publishes its slab and sk_reduce_kernel /
+                         // sk_dz_reduce_kernel sum a tile's slabs and run its epilogue
+  int sk_half;           // split-K forward of a 2-byte plan: fp16 partial tiles,
                          // half the slab bytes written and re-read (sk_fixup: fragment pairs of a
                          // lane in 16-B units)
 };
@@ -146,7 +143,7 @@ struct KStream {
 // staged transposed in LDS, then written row-major into slot (mt, nt) with 16-B stores
 // (rows via ds_read_b64_tr_b16) and, for a mirrored tile, into the lower-triangular slot.
 // ------------------------------------------------------------------------------------
-template <typename T, int NW, int NMI = 8, bool PERM = true>
+template <typename T, int NW, int NMI = 8>
 __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&rb)[NMI], const int (&cb)[4],
                                               int row_base, int col_base, int mt, int nt, int kind,
                                               lds_char* lds, const SimParams& p, int lane) {
@@ -173,7 +170,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
   T* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
   T* mirror = nullptr;
-  if ((kind == kTileSymOff && !p.no_mirror) || kind == kTileDiagUp)  // (kTileDiagUp: the same tile's slot)
+  if (kind == kTileSymOff || kind == kTileDiagUp)  // (kTileDiagUp: the same tile's slot)
     mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
   else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
     const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
@@ -294,20 +291,15 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
       u[2] = (unsigned short)hi[0] | ((unsigned)(unsigned short)hi[1] << 16);
       u[3] = (unsigned short)hi[2] | ((unsigned)(unsigned short)hi[3] << 16);
-      if constexpr (PERM) {
-        // lanes i + 16 g hold 16-byte chunk g of row c0 + i: permute so that lane 4 i + g holds it,
-        // and each 4-lane quad stores one contiguous 64-byte row segment (one row per quad
-        // instead of four: a quad spanning four rows cost the store path ~4x its cycles)
-        const int src = ((lane >> 2) + 16 * (lane & 3)) << 2;
-        u32x4 v;
+      // lanes i + 16 g hold 16-byte chunk g of row c0 + i: permute so that lane 4 i + g holds it,
+      // and each 4-lane quad stores one contiguous 64-byte row segment (one row per quad
+      // instead of four: a quad spanning four rows cost the store path ~4x its cycles)
+      const int src = ((lane >> 2) + 16 * (lane & 3)) << 2;
+      u32x4 v;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)u[k]);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + (lane >> 2)) * (kTile * 2) +
-                                  (col_base + (blk / RB) * 32 + 8 * (lane & 3)) * 2) = v;
-      } else {
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + i) * (kTile * 2) +
-                                  (col_base + r0) * 2) = u;
-      }
+      for (int k = 0; k < 4; ++k) v[k] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)u[k]);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + (lane >> 2)) * (kTile * 2) +
+                                (col_base + (blk / RB) * 32 + 8 * (lane & 3)) * 2) = v;
     }
   }
 }
@@ -480,7 +472,7 @@ __device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[8][4], const SimParams& p,
   const int b1 = (int)(((long long)(stile + 1) * nk - 1) / p.ipb);
   auto slot_off = [&](int bb) {  // byte offset of block bb's slab for this tile
     const long long s = (long long)bb * p.ipb;
-    const bool first_partial = p.sk_out != 2 && (s / nk == stile) && (s % nk != 0);
+    const bool first_partial = !p.splitk && (s / nk == stile) && (s % nk != 0);
     return (unsigned)((2 * bb + (first_partial ? 0 : 1)) * (kTileElems * 4));
   };
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs, 0, 2 * G * kTileElems * 4, 0x00020000);
@@ -510,7 +502,7 @@ __device__ __forceinline__ bool sk_fixup(f32x4 (&acc)[8][4], const SimParams& p,
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
-  if (p.sk_out) return false;  // split-K: the reduce launch finishes the tile
+  if (p.splitk) return false;  // split-K: the reduce launch finishes the tile
   int* flag = reinterpret_cast<int*>(smem);
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(p.sk_cnt + stile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -945,7 +937,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       ke = nk;
       return true;
     }
-    if (p.sk_out == 2) {  // piece-major aligned split: one piece per block
+    if (p.splitk) {  // piece-major aligned split: one piece per block
       if (item > 0) return false;
       stile = bid % p.sk_tiles;
       kb = (int)((bid / p.sk_tiles) * p.ipb);
@@ -985,7 +977,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // Forward streaming needs whole-tile items with an even number of >= 2 K-steps (the streams
   // run two K-steps into the next item; even: its K-step 0 lands in buffer 0, as after a
   // prologue).
-  const bool streaming = kStreamMode && p.fwd_stream && p.sk_tiles == 0 && nk >= 2 && (nk & 1) == 0;
+  const bool streaming = kStreamMode && p.sk_tiles == 0 && nk >= 2 && (nk & 1) == 0;
   bool streamed = false;  // this item's first two K-steps were staged by the previous item
   for (int item = 0;; ++item) {
   int tile, kb, ke, stile;
@@ -1310,7 +1302,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 // (canonical fragment order: 16 fragments of 512 B) -> C into the coefficient buffer. 9 KiB of
 // LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound), and 16
 // waves per tile keep a small problem's few tiles (36 at B = 1024/view) spread over the chip.
-template <typename T, bool PERM = true, bool Q8 = false>
+template <typename T, bool Q8 = false>
 __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   __shared__ __attribute__((aligned(16))) char smem[Q8 ? 2 * 64 * 80 : (sizeof(T) == 2 ? kCoefWaveLds : 16)];
   const int lane = threadIdx.x;
@@ -1354,314 +1346,12 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   if constexpr (Q8)
     coef_epilogue_q8<T>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, kind, (lds_char*)smem, p, lane);
   else
-    coef_epilogue<T, 1, 4, PERM>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, kind, (lds_char*)smem, p, lane);
+    coef_epilogue<T, 1, 4>(acc, rb, cb, 128 * wm + 64 * half, 64 * wn, t.x, t.y, kind, (lds_char*)smem, p, lane);
 }
 
-// ------------------------------------------------------------------------------------
-// Diagonal-tile strips: the remainder of the forward's whole rounds (launch_fwd_stats).
-// A diagonal tile S_tt is symmetric, so its row partials are all the epilogue owes and its
-// 16-row strips are independent: one 4-wave block per strip (16 blocks per tile), wave w owns
-// columns [64w, 64w + 64) (4 fragments of 16x16) and runs on its own: it LDS-DMAs the strip's
-// 16 A rows and its 64 B rows (80 rows x 128 B per K-step, whole lines, 8 rows per instruction)
-// into its private 3-stage ring and reads the fragments back with conflict-free ds_read_b128
-// (chunk ^ ((row >> 1) & 7) swizzle on the source address, as the GEMM). Only the wave's own
-// counted vmcnt orders its reads behind its DMA, so the K loop has no barrier. (Fragment-shaped
-// loads straight to registers put 16 rows in every instruction's 16 lanes and ran 4x slower.)
-// Row partials are merged over the 4 waves in LDS; masks, the fixed-shift / per-row-max
-// partials and the kept-cosine layout are the GEMM epilogue's.
-// ------------------------------------------------------------------------------------
-// NST = ring depth: 3 stages (120 KiB, one block per CU) when the strips fit in one wave of
-// blocks, 2 (80 KiB, two blocks per CU) when there are more strips than CUs. The row-partial
-// merge reuses wave 0's ring after every wave has left its K loop.
-constexpr int kStripRows = 80;                                   // 16 A rows + 64 B rows per wave
-constexpr int kStripStage = kStripRows * kKStepBytes;            // 10 KiB
-
-template <typename T, int FX, int NST>
-__global__ __launch_bounds__(256) void diag_strip_kernel(const SimParams p) {
-  constexpr int kStripStages = NST;
-  constexpr int kStripWaveLds = kStripStages * kStripStage;
-  constexpr int kStripLds = 4 * kStripWaveLds;
-  using MM = Mfma<T>;
-  typedef typename MM::frag frag;
-  typedef typename StoreT<T>::type TS;
-  typedef __attribute__((address_space(3))) const frag lds_frag;
-  // one LDS array (a second __shared__ object makes hipcc drain the LDS-DMA before ds_reads)
-  __shared__ __attribute__((aligned(16))) char smem[kStripLds];
-  lds_char* lds = (lds_char*)smem;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 strips share one XCD's L2
-  const int tile = idx >> 4, strip = idx & 15;
-  const int4 t = p.tiles[tile];
-  const int mt = t.x, nt = t.y;
-  const int nk = (int)(p.kbytes / kKStepBytes);
-  // DMA piece j (j < 10) = ring rows [8j, 8j + 8): rows 0-15 the strip's A rows, 16-79 this
-  // wave's B rows; lane -> row 8j + (lane >> 3), 16-byte chunk (lane & 7) ^ ((row >> 1) & 7)
-  const char* src[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int row = 8 * j + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    src[j] = row < 16 ? p.A.base + (long long)mt * p.A.row_tile_stride + (long long)(16 * strip + row) * p.A.ld + 16 * chunk
-                      : p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride +
-                            (long long)(64 * w + row - 16) * p.B.ld + 16 * chunk;
-  }
-  lds_char* ring = lds + w * kStripWaveLds;
-  auto stage = [&](int s, int buf) {
-    const long long o = (long long)s * kKStepBytes;
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + o), (lds_void*)(ring + buf * kStripStage + j * 8 * kKStepBytes),
-                                       16, 0, 0);
-  };
-  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
-  f32x4 acc[4];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // prologue: steps 0 .. NST-1 (clamped: trailing prefetches re-read the last step)
-#pragma unroll
-  for (int i = 0; i < kStripStages; ++i) stage(i < nk ? i : nk - 1, i);
-  int buf = 0;
-  for (int s = 0; s < nk; ++s) {
-    // step s landed (the NST - 1 younger steps' 10 pieces each still in flight)
-    if constexpr (kStripStages == 3) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    const lds_char* st = ring + buf * kStripStage;
-    frag af[2], bf[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int pch = ((4 * c + cq) ^ sw) << 4;
-      af[c] = *(lds_frag*)(st + r16 * kKStepBytes + pch);
-#pragma unroll
-      for (int f = 0; f < 4; ++f) bf[c][f] = *(lds_frag*)(st + (16 + 16 * f + r16) * kKStepBytes + pch);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done: the stage may be refilled
-    __builtin_amdgcn_sched_barrier(0);
-    const int nx = s + kStripStages;
-    stage(nx < nk ? nx : nk - 1, buf);
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) acc[f] = MM::mma(af[c], bf[c][f], acc[f]);
-    buf = buf == kStripStages - 1 ? 0 : buf + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
-  // lane holds S[row 16 strip + 4 (lane >> 4) + r][col 64 w + 16 f + (lane & 15)] (tile-local)
-  const int rb0 = 16 * strip;
-  if (p.sc) {  // kept cosines, canonical fragment order (sc_unit), before the masks
-    TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-    if constexpr (sizeof(TS) == 2) {
-#pragma unroll
-      for (int np = 0; np < 2; ++np) {
-        union { TS h[8]; u32x4 u; } pk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pk.h[r] = from_f32<TS>(acc[2 * np][r]);
-          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r]);
-        }
-        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * w + 32 * np, lane) * 8) = pk.u;
-      }
-    } else {
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * w + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f];
-    }
-  }
-  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
-  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
-  const float sc_ = p.acc_scale, M = p.y_scale;
-  float2 part[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int tr = rb0 + 4 * (lane >> 4) + r, gi = r0 + tr;
-    float y[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int tc = 64 * w + 16 * f + (lane & 15), d = tc - tr;
-      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
-                        ((d == D2) & (gi >= p.n_half));
-      y[f] = drop ? kNegInf : acc[f][r] * sc_;
-    }
-    if constexpr (FX != 0) {
-      float s = (fast_exp2(y[0] - M) + fast_exp2(y[1] - M)) + (fast_exp2(y[2] - M) + fast_exp2(y[3] - M));
-      s = row16_sum(s);
-      part[r] = make_float2(s > 0.f ? M : kNegInf, s);
-    } else {
-      float m = fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3]));
-      m = row16_max(m);
-      const float ms = (m == kNegInf) ? 0.f : m;
-      float s = (fast_exp2(y[0] - ms) + fast_exp2(y[1] - ms)) + (fast_exp2(y[2] - ms) + fast_exp2(y[3] - ms));
-      s = row16_sum(s);
-      part[r] = make_float2(m, s);
-    }
-  }
-  typedef __attribute__((address_space(3))) float lds_fl;
-  lds_fl* red = (lds_fl*)lds;  // [4 waves][16 rows] x (max, sum), over wave 0's drained ring
-  __syncthreads();
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      red[2 * (w * 16 + 4 * (lane >> 4) + r)] = part[r].x;
-      red[2 * (w * 16 + 4 * (lane >> 4) + r) + 1] = part[r].y;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < 16) {
-    const int i = threadIdx.x;
-    float m = red[2 * i], s = red[2 * i + 1];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) lse_merge(m, s, red[2 * (q * 16 + i)], red[2 * (q * 16 + i) + 1]);
-    p.part[(long long)nt * p.Rpad + r0 + rb0 + i] = make_float2(m, s);
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Diagonal tiles as 64x64 sub-tiles (the forward's whole-round remainder, alternative to the
-// 16-row strips): 16 blocks per tile, block (a, b) computes S[64a.., 64b..] with a 3-stage LDS
-// ring shared by its 4 waves (64 A + 64 B rows per K-step, one barrier per step), wave w rows
-// 64a + 16w.. x all 64 columns. A block reads 128 rows per K-step instead of a strip block's
-// 4 x 80, so the L2 -> CU traffic is 2.5x smaller. Row partials over the sub-tile's 64 columns
-// go to write-through scratch rows[tile][a][b][64]; the 4th block of a row group (ticket) merges
-// them in b order (deterministic). Masks, partial forms and kept cosines as the GEMM epilogue.
-// ------------------------------------------------------------------------------------
-// 3 stages (49 KiB: 3 blocks per CU fit, which the 512 sub-tiles of config 5 need); a 6-stage
-// ring (5 K-steps in flight) measured the same at the headline (profiles/r2/subtiles): the loop
-// is bound by the per-step LDS-DMA issue and barrier, not by load latency.
-constexpr int kSubStage = 128 * kKStepBytes;   // 64 A + 64 B rows = 16 KiB
+// Ring of the diagonal-remainder kernel below: a stage holds 64 A + 64 B rows of one K-step.
+constexpr int kSubStage = 128 * kKStepBytes;   // 16 KiB
 constexpr int kSubStages = 3;
-constexpr int kSubLds = kSubStages * kSubStage + 1024;  // + the ticket flag
-template <typename T, int FX>
-__global__ __launch_bounds__(256) void diag_sub_kernel(const SimParams p, float2* __restrict__ scratch) {
-  using MM = Mfma<T>;
-  typedef typename MM::frag frag;
-  typedef typename StoreT<T>::type TS;
-  typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[kSubLds];  // one array (see diag_strip_body)
-  lds_char* lds = (lds_char*)smem;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 sub-tiles share one XCD
-  const int tile = idx >> 4, a = (idx >> 2) & 3, b = idx & 3;
-  const int4 t = p.tiles[tile];
-  const int mt = t.x, nt = t.y;
-  const int nk = (int)(p.kbytes / kKStepBytes);
-  // DMA piece j of wave w: ring rows 32w + 8j + (lane >> 3) (rows 0-63 A = tile rows 64a..,
-  // 64-127 B = tile columns 64b..), 16-byte chunk (lane & 7) ^ ((row >> 1) & 7)
-  const char* src[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = 32 * w + 8 * j + (lane >> 3);
-    const int chunk = (lane & 7) ^ ((row >> 1) & 7);
-    src[j] = row < 64 ? p.A.base + (long long)mt * p.A.row_tile_stride + (long long)(64 * a + row) * p.A.ld + 16 * chunk
-                      : p.B.base + (long long)(nt - p.b_tile0) * p.B.row_tile_stride +
-                            (long long)(64 * b + row - 64) * p.B.ld + 16 * chunk;
-  }
-  auto stage = [&](int s, int buf) {
-    const long long o = (long long)s * kKStepBytes;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src[j] + o),
-                                       (lds_void*)(lds + buf * kSubStage + (32 * w + 8 * j) * kKStepBytes), 16, 0, 0);
-  };
-  const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
-  f32x4 acc[4];
-#pragma unroll
-  for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int P = kSubStages - 1;  // K-steps in flight
-#pragma unroll
-  for (int i = 0; i < P; ++i) stage(i < nk ? i : nk - 1, i);
-  int buf = 0;
-  for (int s = 0; s < nk; ++s) {
-    // own pieces of step s landed (the P - 1 younger steps' 4 each in flight); after the
-    // barrier every wave's have, and every wave has finished reading the buffer refilled next
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    static_assert(4 * (P - 1) == 4, "vmcnt count = pieces per step x (P - 1)");
-    __builtin_amdgcn_s_barrier();
-    const int nb2 = buf == 0 ? kSubStages - 1 : buf - 1;  // (s + P) % kSubStages
-    stage(s + P < nk ? s + P : nk - 1, nb2);
-    const lds_char* st = lds + buf * kSubStage;
-    frag af[2], bf[2][4];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int pch = ((4 * c + cq) ^ sw) << 4;
-      af[c] = *(lds_frag*)(st + (16 * w + r16) * kKStepBytes + pch);
-#pragma unroll
-      for (int f = 0; f < 4; ++f) bf[c][f] = *(lds_frag*)(st + (64 + 16 * f + r16) * kKStepBytes + pch);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) acc[f] = MM::mma(af[c], bf[c][f], acc[f]);
-    buf = buf == kSubStages - 1 ? 0 : buf + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
-  // lane holds S[row 64a + 16w + 4 (lane >> 4) + r][col 64b + 16 f + (lane & 15)] (tile-local)
-  const int rb0 = 64 * a + 16 * w;
-  if (p.sc) {  // kept cosines, canonical fragment order, before the masks
-    TS* sto = reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems;
-    if constexpr (sizeof(TS) == 2) {
-#pragma unroll
-      for (int np = 0; np < 2; ++np) {
-        union { TS h[8]; u32x4 u; } pk;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pk.h[r] = from_f32<TS>(acc[2 * np][r]);
-          pk.h[4 + r] = from_f32<TS>(acc[2 * np + 1][r]);
-        }
-        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * np, lane) * 8) = pk.u;
-      }
-    } else {
-#pragma unroll
-      for (int f = 0; f < 4; ++f)
-        *reinterpret_cast<f32x4*>(sto + (((rb0 >> 4) * 16 + ((64 * b + 16 * f) >> 4)) * 64 + lane) * 4) = acc[f];
-    }
-  }
-  const int r0 = mt * kTile, c0 = (nt * kTile) % p.Rpad;
-  const int D0 = r0 - c0, D1 = D0 + p.n_half, D2 = D0 - p.n_half;
-  const float sc_ = p.acc_scale, M = p.y_scale;
-  const auto srs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + a) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int tr = rb0 + 4 * (lane >> 4) + r, gi = r0 + tr;
-    float y[4];
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int tc = 64 * b + 16 * f + (lane & 15), d = tc - tr;
-      const bool drop = (gi >= p.R) | (c0 + tc >= p.R) | (d == D0) | ((d == D1) & (gi < p.n_half)) |
-                        ((d == D2) & (gi >= p.n_half));
-      y[f] = drop ? kNegInf : acc[f][r] * sc_;
-    }
-    float m = M;
-    if constexpr (!FX) m = row16_max(fmaxf(fmaxf(y[0], y[1]), fmaxf(y[2], y[3])));
-    const float ms = (m == kNegInf) ? 0.f : m;
-    float sr = (fast_exp2(y[0] - ms) + fast_exp2(y[1] - ms)) + (fast_exp2(y[2] - ms) + fast_exp2(y[3] - ms));
-    sr = row16_sum(sr);
-    const float mo = FX ? (sr > 0.f ? M : kNegInf) : m;
-    if ((lane & 15) == 0)  // write-through: merged by the row group's last block on any XCD
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mo), __float_as_uint(sr)}, srs,
-                                            (b * 64 + 16 * w + 4 * (lane >> 4) + r) * 8, 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem + kSubStages * kSubStage);
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(p.sk_cnt + tile * 4 + a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == 3;
-    if (last) __hip_atomic_store(p.sk_cnt + tile * 4 + a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0] || threadIdx.x >= 64) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-  const int i = threadIdx.x;
-  u32x2 q[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) q[k] = __builtin_amdgcn_raw_buffer_load_b64(srs, (k * 64 + i) * 8, 0, 16);
-  float m = __uint_as_float(q[0][0]), s = __uint_as_float(q[0][1]);
-#pragma unroll
-  for (int k = 1; k < 4; ++k) lse_merge(m, s, __uint_as_float(q[k][0]), __uint_as_float(q[k][1]));
-  p.part[(long long)nt * p.Rpad + r0 + 64 * a + i] = make_float2(m, s);
-}
 
 // ------------------------------------------------------------------------------------
 // Diagonal tiles by their upper 64x64 regions only (the coefficient pass mirrors a diagonal
@@ -1673,7 +1363,8 @@ __global__ __launch_bounds__(256) void diag_sub_kernel(const SimParams p, float2
 // slab, as sk_fixup) and runs the epilogue: kept cosines of (a, b), masks, row partials of group
 // a over b's 64 columns and column partials of group b over a's 64 rows (the mirrored region's
 // row partials). The 4th contribution to a row group (ticket) merges the 4 in b order, so the
-// result does not depend on arrival order. Half the L2 -> CU bytes of diag_sub_kernel; the
+// result does not depend on arrival order. Half the L2 -> CU bytes of a full 16-region split
+// (and 2.5x fewer than 16-row strips, the round-2 form: profiles/r3/diag_up); the
 // loop is bound by load latency over the few K-steps in flight, so the diagonal-region blocks
 // (half the rows per K-step) run a 6-stage ring of 8 KiB stages in the same LDS (5 in flight).
 // ------------------------------------------------------------------------------------
@@ -1684,7 +1375,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   typedef typename MM::frag frag;
   typedef typename StoreT<T>::type TS;
   typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array (see diag_strip_body)
+  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   lds_char* lds = (lds_char*)smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nt_d = gridDim.x >> 4;                    // diagonal tiles in this launch
@@ -1896,7 +1587,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
 // ------------------------------------------------------------------------------------
 // Split-K forward for tile-starved launches (fewer tiles than CUs, long K: BASELINE config 4,
 // 36 tiles x 128 K-steps): every K piece of the persistent GEMM publishes its fp32 partial tile
-// (sk_out), and this launch sums each tile's pieces (fixed block order: deterministic) and runs
+// (SimParams::splitk), and this launch sums each tile's pieces (fixed block order: deterministic) and runs
 // the forward epilogue in 16 row strips per tile instead of one last-arriving block per tile
 // reading all p - 1 slabs serially. A strip block writes its rows' partials (complete over the
 // tile) and the kept cosines; for a kTileSymOff tile it also publishes its 16-row column
@@ -1924,12 +1615,8 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
   const int s16 = 16 * strip;
   const int nk = p.nk;
   const long long ipb = p.ipb;
-  // the tile's pieces: contiguous blocks b0..b1 (tile-major split) or blocks pc * sk_tiles + tile,
-  // pc = 0 .. npc - 1 (piece-major aligned split, sk_out == 2); summed in piece order
-  const bool pm = p.sk_out == 2;
-  const int npc = pm ? (int)((nk + ipb - 1) / ipb) : 0;
-  const int b0 = pm ? 0 : (int)((long long)tile * nk / ipb);
-  const int b1 = pm ? npc - 1 : (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  // the tile's pieces: blocks pc * sk_tiles + tile, pc = 0 .. npc - 1, summed in piece order
+  const int b0 = 0, b1 = (int)((nk + ipb - 1) / ipb) - 1;
   // this thread's 4 fragments (s16, cb[j] = 64 w + 16 j), MFMA C layout: rows s16 + r4 + r,
   // column cb[j] + c1; a wave reads 1 KiB contiguous per fragment and slab
   const int r4 = 4 * (lane >> 4), c1 = lane & 15;
@@ -1940,13 +1627,8 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
-  auto slab = [&](int bb) {  // bb: block (tile-major) or piece (piece-major)
-    if (pm) return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems;
-    const long long st = (long long)bb * ipb;
-    const bool first_partial = (st / nk == tile) && (st % nk != 0);
-    return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
-  };
-  if (pm && p.sk_half) {
+  auto slab = [&](int bb) { return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems; };  // piece bb
+  if (p.sk_half) {
     // fp16 slabs (sk_fixup): fragments j = 2 jp, 2 jp + 1 of this thread are one 16-B unit, at
     // ((W * 16 + f / 2) * 64 + lane) of the slab for the float offset ((W * 32 + f) * 64 + lane) * 4
     unsigned hoff[2];
@@ -2089,7 +1771,7 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
 
 // ------------------------------------------------------------------------------------
 // Split-K dZ for tile-starved dZ GEMMs (d <= 1024 at 8192 rows: 64 tiles x 128 K-steps on 256
-// CUs): the K pieces publish fp32 partial tiles (sk_out) and this launch sums each tile's
+// CUs): the K pieces publish fp32 partial tiles (SimParams::splitk) and this launch sums each tile's
 // pieces in block order (deterministic) and writes the dZ tile exactly as the GEMM's epilogue
 // would (fp16 or fp32, optionally accumulated), 64 blocks per tile: block (w, k) = fragments
 // 4k..4k+3 of GEMM wave w, one (fragment, lane) per thread (one batch of slab loads in flight).
@@ -2100,18 +1782,10 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
   const int mt = t.x, nt = t.y;
   const int nk = p.nk;
   const long long ipb = p.ipb;
-  // the tile's pieces: tile-major contiguous blocks b0..b1, or piece-major (sk_out == 2, see
-  // sk_reduce_kernel): piece pc is block pc * sk_tiles + tile
-  const bool pm = p.sk_out == 2;
-  const int b0 = pm ? 0 : (int)((long long)tile * nk / ipb);
-  const int b1 = pm ? (int)((nk + ipb - 1) / ipb) - 1 : (int)(((long long)(tile + 1) * nk - 1) / ipb);
+  // the tile's pieces (piece-major, as sk_reduce_kernel): piece pc is block pc * sk_tiles + tile
+  const int b0 = 0, b1 = (int)((nk + ipb - 1) / ipb) - 1;
   const float* slabs = reinterpret_cast<const float*>(p.sk_slabs);
-  auto slab = [&](int bb) {
-    if (pm) return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems;
-    const long long st = (long long)bb * ipb;
-    const bool first_partial = (st / nk == tile) && (st % nk != 0);
-    return slabs + (size_t)(2 * bb + (first_partial ? 0 : 1)) * kTileElems;
-  };
+  auto slab = [&](int bb) { return slabs + (size_t)(2 * (bb * p.sk_tiles + tile) + 1) * kTileElems; };
   const int wa = w >> 2, wb = w & 3;
   // one output fragment f of GEMM wave w for this lane, summed over the pieces (v)
   auto emit = [&](int f, int lane, f32x4 v) {
@@ -2160,35 +1834,6 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
       *o = p.accum ? *o + v : v;
     }
   };
-  if (pm && p.sk_half) {
-    // fp16 slabs (sk_fixup): one 16-B unit = fragments 2 q, 2 q + 1 of a lane; blocks kq < 4
-    // cover the wave's 16 x 64 units, one unit (two fragments) per thread
-    if (kq >= 4) return;
-    const int u = threadIdx.x + 256 * kq, q = u >> 6, lane = u & 63;
-    const size_t hoff = (size_t)((w * 16 + q) * 64 + lane) * 16;
-    f32x4 v0 = f32x4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
-    for (int bb = b0; bb <= b1; bb += 4) {  // 4 slab loads in flight (clamped, weighted)
-      u32x4 x[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        x[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-            reinterpret_cast<const char*>(slab(bb + k <= b1 ? bb + k : b1)) + hoff));
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float wt = bb + k <= b1 ? 1.f : 0.f;
-        union { u32x4 u; _Float16 h[8]; } pk;
-        pk.u = x[k];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v0[r] += (float)pk.h[r] * wt;
-          v1[r] += (float)pk.h[4 + r] * wt;
-        }
-      }
-    }
-    emit(2 * q, lane, v0);
-    emit(2 * q + 1, lane, v1);
-    return;
-  }
   {
     const int u = threadIdx.x + 256 * kq, f = u >> 6, lane = u & 63;
     const int off = ((w * 32 + f) * 64 + lane) * 4;

@@ -47,14 +47,12 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
     nch_ = sym_num_chunks(g_.row_tiles);
     ccs_ = bwd_ == DType::F32 ? 4 : 2;
   }
-  // dZ straight from the upper-triangular C and the (gathered) Zq rows: no ZqT, no mirrors
   q8_ = !small_ && fp8_backward_eligible(g_, cfg.compute) &&
         (cfg.fp8_backward < 0 ? fp8_backward_enabled() : cfg.fp8_backward != 0);
-  sym_ = !small_ && !q8_ && !symm_ && cfg.dz_sym && dz_sym_enabled() && dz_sym_eligible(g_, cfg.compute);
   // normalisation backward fused into the dZ epilogue (the coefficient pass emits dot partials;
   // the symmetric mode sums received contributions in launch_norm_bwd instead)
   // (not on fp8 plans: dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines, ~1e-2 off)
-  fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && norm_fuse_enabled() && g_.dim % 8 == 0;
+  fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && g_.dim % 8 == 0;
 
   const auto ft = symm_ ? build_sym_fwd_tiles(g_, jobs_, nch_) : build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -69,7 +67,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   const std::vector<Slot> slots = {
       {(void**)&zq_all_, W * Rp * g_.ld_k * cs_},
       {(void**)&zq8_all_, f8_ ? W * Rp * g_.ld_k8 : 0},
-      {(void**)&zqt_all_, (sym_ || q8_) ? 0 : W * g_.dim_n * g_.ld_t * cs_},
+      {(void**)&zqt_all_, q8_ ? 0 : W * g_.dim_n * g_.ld_t * cs_},
       {(void**)&zq8t_, q8_ ? (size_t)g_.dim_n * (size_t)q8_ldt(g_) : 0},
       {(void**)&q8_mneg_, q8_ ? Rp * 4 : 0},
       {(void**)&q8_lmin_, q8_ ? (size_t)4 : (size_t)0},
@@ -165,7 +163,7 @@ void Engine::forward(const void* h, hipStream_t s) {
     }
     launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
     // world 1: the transpose is written by the LSE launch (beside the merge, see below)
-    if (world_ > 1 && !sym_) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
+    if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
@@ -173,10 +171,8 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_prep_, 0));
     comm_->all_gather(op_local, op_all, op_bytes, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zq_, comm_stream_));
-    // the backward's B operand: ZqT blocks, or (dz_sym) the fp16 rows themselves — already
-    // gathered above unless the forward ran on the fp8 copy
-    if (!sym_) comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
-    else if (f8_) comm_->all_gather(zq_local, zq_all_, Rp * g_.ld_k * cs_, comm_stream_);
+    // the backward's B operand: the ZqT blocks
+    comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
     zqt_pending_ = true;
   }
@@ -204,7 +200,7 @@ void Engine::forward(const void* h, hipStream_t s) {
       q8.lmin = q8_lmin_;
       q8.zq8t = zq8t_;
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
-    } else if (world_ == 1 && !sym_)
+    } else if (world_ == 1)
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
     else
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
@@ -241,8 +237,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");
     if (cfg_.keep_cos)
-      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr,
-                  /*upper_only=*/sym_ && !std::getenv("NTXENT_DZSYM_NOMIR"), dotp_, q8_ ? &q8 : nullptr);
+      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr, dotp_, q8_ ? &q8 : nullptr);
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
@@ -263,12 +258,10 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     nf.grad_out = grad_out ? grad_out : one_;
     nf.dh = dh;
     const bool fused =
-        sym_ ? launch_dz_sym(cfg_.compute, cbuf_, zq_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
-                             fuse_ ? &nf : nullptr)
-        : q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
-                          fuse_ ? &nf : nullptr, &q8, cpos_)
-             : launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32,
-                         fuse_ ? &nf : nullptr);
+        q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
+                        fuse_ ? &nf : nullptr, &q8, cpos_)
+            : launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32,
+                        fuse_ ? &nf : nullptr);
     if (fused) return;  // dh written by the dZ epilogue
   }
   {

@@ -73,7 +73,8 @@ const int4* Engine::dz_rows(int m0, int m1) const {
 // tiles from tile a_tile0 (row panels a_panel_tiles tiles apart), K = k_tiles * 256 columns of
 // the ZqT blocks from block b_block0, column b_col0 (a K range past one block covers whole blocks).
 void Engine::dz_view(const char* abuf, long a_tile0, long a_panel_tiles, const char* bbuf, int b_block0, long b_col0,
-                     int k_tiles, int m0, int m1, void* out, bool accum, bool out_f16, hipStream_t s) {
+                     int k_tiles, int m0, int m1, void* out, bool accum, bool out_f16, hipStream_t s,
+                     const GemmWorkspace& ws) {
   if (m1 <= m0 || k_tiles == 0) return;
   const long blk = (long)g_.dim_n * g_.ld_t;
   const long kcols = (long)k_tiles * kTile;
@@ -85,7 +86,7 @@ void Engine::dz_view(const char* abuf, long a_tile0, long a_panel_tiles, const c
   const char* a = abuf + (size_t)a_tile0 * kTileElems * cs_;
   const char* b = bbuf + ((size_t)b_block0 * blk + b_col0) * cs_;
   launch_dz_view(bwd_, a, a_panel_tiles, b, kblk_cols, blk, k_tiles, dz_rows(m0, m1), (m1 - m0) * (g_.dim_n / kTile),
-                 out, accum, ws_, g_, s, out_f16);
+                 out, accum, ws, g_, s, out_f16);
 }
 
 void Engine::forward_sym(const void* h, hipStream_t s) {
@@ -202,12 +203,12 @@ void Engine::backward_sym(const float* grad_out, void* dh, hipStream_t s) {
   {
     NTXENT_TRACE("ntxent.dz_partners");
     fault_point("dz");
-    if (nfull_ > 0) dz_view(mbuf_, 0, rt, zqt_all_, r, 0, rt, 0, nfull_ * rt, contrib_, false, f16c, s);
+    if (nfull_ > 0) dz_view(mbuf_, 0, rt, zqt_all_, r, 0, rt, 0, nfull_ * rt, contrib_, false, f16c, s, ws_);
     if ((int)jobs_.size() > nfull_) {
       const SymJob& sp = jobs_.back();
       const int slot = ((sp.q - r - 1) % W + W) % W;
       dz_view(mbuf_, (long)slot * rt * rt + sp.m0, rt, zqt_all_, r, (long)sp.m0 * kTile, sp.m1 - sp.m0, sp.k0, sp.k1,
-              contrib_ + (size_t)nfull_ * slab * ccs_, false, f16c, s);
+              contrib_ + (size_t)nfull_ * slab * ccs_, false, f16c, s, ws_);
     }
   }
   // point to point: contributions out, the partners' contributions to my rows in (fp32 plans:
@@ -232,17 +233,17 @@ void Engine::backward_sym(const float* grad_out, void* dh, hipStream_t s) {
     // own contributions while the partners' travel: C_{r,r} Z_r + the full blocks (consecutive
     // rank blocks r .. r+nfull, two GEMMs if they wrap) + the split block's rows
     NTXENT_TRACE("ntxent.dz_own");
-    GemmWorkspace keep = ws_;
-    ws_.sched_cus = std::max(1, ws_.num_cus - std::min(cfg_.comm_reserve_cus, ws_.num_cus / 2));
+    // (a local workspace view: the member stays untouched whatever these launches throw)
+    GemmWorkspace ws_ovl = ws_;
+    ws_ovl.sched_cus = std::max(1, ws_.num_cus - std::min(cfg_.comm_reserve_cus, ws_.num_cus / 2));
     const int nb = 1 + nfull_, first = std::min(nb, W - r);
-    dz_view(cbuf_, (long)r * rt, ct, zqt_all_, r, 0, first * rt, 0, rt, slabs_, false, false, s);
-    if (nb > first) dz_view(cbuf_, 0, ct, zqt_all_, 0, 0, (nb - first) * rt, 0, rt, slabs_, true, false, s);
+    dz_view(cbuf_, (long)r * rt, ct, zqt_all_, r, 0, first * rt, 0, rt, slabs_, false, false, s, ws_ovl);
+    if (nb > first) dz_view(cbuf_, 0, ct, zqt_all_, 0, 0, (nb - first) * rt, 0, rt, slabs_, true, false, s, ws_ovl);
     if ((int)jobs_.size() > nfull_) {
       const SymJob& sp = jobs_.back();
       dz_view(cbuf_, (long)sp.q * rt + sp.k0, ct, zqt_all_, sp.q, (long)sp.k0 * kTile, sp.k1 - sp.k0, sp.m0, sp.m1, slabs_,
-              true, false, s);
+              true, false, s, ws_ovl);
     }
-    ws_ = keep;
   }
   NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_cdone_, 0));
   {

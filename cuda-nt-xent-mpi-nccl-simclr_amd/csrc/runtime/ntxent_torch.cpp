@@ -67,7 +67,6 @@ struct Plan {
   int n_dz = 0;
   int num_cus = 256;
   bool small = false;  // single-rank small-problem path (kernels/small_kernels.hip)
-  bool dz_sym = false;  // dZ from the upper-triangular C and Zq itself (launch_dz_sym)
 
   int rows() const { return g.rows; }
   int rows_pad() const { return g.rows_pad; }
@@ -96,11 +95,9 @@ static at::Tensor upload_tiles(const std::vector<int4>& v, int device) {
 std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double temperature,
                                const std::string& compute, int device) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int, float, int, int, int>, std::shared_ptr<Plan>> cache;
+  static std::map<std::tuple<int, int, int, int, float, int, int>, std::shared_ptr<Plan>> cache;
   const DType comp = choose_compute(at::kFloat, compute != "fp32" && compute != "float32", compute);
-  // the tile order is part of the plan (its tile lists): a toggled order gets its own plan
-  auto key = std::make_tuple(rows, dim, world, rank, (float)temperature, (int)comp, device,
-                             (int)superblock_order_enabled());
+  auto key = std::make_tuple(rows, dim, world, rank, (float)temperature, (int)comp, device);
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
@@ -118,7 +115,6 @@ std::shared_ptr<Plan> get_plan(int rows, int dim, int world, int rank, double te
   p->n_dz = (int)dt.size();
   p->dz_tiles = upload_tiles(dt, device);
   p->small = small_path_eligible(p->g, comp);
-  p->dz_sym = dz_sym_eligible(p->g, comp);
   cache.emplace(key, p);
   return p;
 }
@@ -154,12 +150,13 @@ static at::Tensor device_scratch(const at::Tensor& like, size_t bytes, int slot)
 }
 
 
-// CUs left free for communication kernels: set_grid_reserve (ntxent.h), see
-// parallel/commstats.py:comm_overlap.
-static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P) {
+// reserve_cus: CUs this launch leaves free for communication kernels that overlap it (a
+// per-launch argument: parallel/commstats.py:comm_reserve_cus), at most half the chip.
+static GemmWorkspace gemm_ws(const at::Tensor& like, int ntiles, const Plan& P, int reserve_cus = 0) {
+  NTXENT_CHECK(reserve_cus >= 0, "reserve_cus must be >= 0");
   GemmWorkspace ws;
   ws.num_cus = P.num_cus;
-  ws.sched_cus = std::max(1, P.num_cus - std::min(grid_reserve(), P.num_cus / 2));
+  ws.sched_cus = std::max(1, P.num_cus - std::min(reserve_cus, P.num_cus / 2));
   ws.bytes = gemm_workspace_bytes(ntiles, P.num_cus);
   ws.ptr = device_scratch(like, ws.bytes, 0).data_ptr();
   return ws;
@@ -247,7 +244,7 @@ std::vector<at::Tensor> fwd_stats(const at::Tensor& zq_local, const at::Tensor& 
 // (sc may be undefined). The own-rank tiles come first (P.n_own of them) and read only this
 // rank's slot of zq_all, so they can run while the rest of zq_all is being gathered.
 void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const Plan& P, at::Tensor& part,
-                     const c10::optional<at::Tensor>& sc, int first, int count) {
+                     const c10::optional<at::Tensor>& sc, int first, int count, int reserve_cus) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   check_input(part, "part");
@@ -260,7 +257,7 @@ void fwd_stats_range(const at::Tensor& zq_local, const at::Tensor& zq_all, const
   if (keep) NTXENT_CHECK(sc->numel() == (long)P.n_fwd * kTileElems, "sc must hold n_fwd tiles");
   if (count == 0) return;
   const at::DeviceGuard guard(zq_local.device());
-  auto ws = gemm_ws(zq_local, count, P);
+  auto ws = gemm_ws(zq_local, count, P, reserve_cus);
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(),
                    reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()) + first, count,
@@ -298,16 +295,15 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
 }
 
 // Kept cosines (compact, one slot per forward tile) -> coefficient buffer (all tiles).
-// upper_only: only the stored tiles (the layout dz_sym reads), no mirrored lower tiles.
 at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
-                bool upper_only = false, float* dotp = nullptr) {
+                float* dotp = nullptr) {
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf), nullptr,
-              upper_only, dotp);
+              dotp);
   return cbuf;
 }
 
@@ -355,27 +351,6 @@ at::Tensor norm_bwd(const at::Tensor& slabs, const at::Tensor& h, const at::Tens
   return dh;
 }
 
-// dZ = C Zq from upper-triangular coefficient tiles (coef(..., upper_only=true) or coef_gemm)
-// and the normalised rows (no ZqT); fp16 slab.
-at::Tensor dz_sym(const at::Tensor& cbuf, const at::Tensor& zq_all, const Plan& P, const NormFuse* nf = nullptr,
-                  bool* fused = nullptr) {
-  check_input(cbuf, "cbuf");
-  check_input(zq_all, "zq_all");
-  NTXENT_CHECK(P.dz_sym, "dz_sym: plan not eligible (see dz_sym_eligible)");
-  NTXENT_CHECK(zq_all.numel() == (long)P.g.world * P.g.rows_pad * P.g.ld_k && zq_all.scalar_type() == to_scalar(P.bwd()),
-               "zq_all must be [world*rows_pad, ld_k] in the backward dtype");
-  NTXENT_CHECK(cbuf.numel() == (long)P.g.row_tiles * P.g.col_tiles * kTileElems && cbuf.scalar_type() == to_scalar(P.bwd()),
-               "cbuf must be [row_tiles * col_tiles] tiles in the backward dtype");
-  const at::DeviceGuard guard(cbuf.device());
-  auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(cbuf, at::kHalf));
-  auto ws = gemm_ws(cbuf, P.n_dz, P);
-  const bool f = launch_dz_sym(P.comp, cbuf.data_ptr(), zq_all.data_ptr(),
-                               reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws,
-                               P.g, cur_stream(cbuf), /*out_f16=*/true, nf);
-  if (fused) *fused = f;
-  return slabs;
-}
-
 // ---- ring-negatives stage ops (O(local) memory; parallel/ring.py) --------------------------
 // `zq_chunk` holds the normalised rows of ONE rank (rows_pad x op_ld): the rank whose global
 // column tiles start at `b_tile0`. `tiles` is an explicit int32 [n, 4] tile list (a subset of
@@ -388,7 +363,7 @@ static const int4* tile_ptr(const at::Tensor& tiles, int& n) {
 }
 
 void fwd_stats_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int b_tile0, const at::Tensor& tiles,
-                     const Plan& P, at::Tensor& part) {
+                     const Plan& P, at::Tensor& part, int reserve_cus) {
   check_input(zq_local, "zq_local");
   check_input(zq_chunk, "zq_chunk");
   check_input(part, "part");
@@ -399,7 +374,7 @@ void fwd_stats_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int
   const int4* tp = tile_ptr(tiles, n);
   if (n == 0) return;
   const at::DeviceGuard guard(zq_local.device());
-  auto ws = gemm_ws(zq_local, n, P);
+  auto ws = gemm_ws(zq_local, n, P, reserve_cus);
   BlockView bv;
   bv.b_tile0 = b_tile0;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_chunk.data_ptr(), tp, n,
@@ -409,7 +384,8 @@ void fwd_stats_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int
 // Coefficient tiles of one column block (recomputed S) into a compact [row_tiles][c_ld] tile
 // buffer whose first column tile is global tile c_tile0.
 at::Tensor coef_gemm_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chunk, int b_tile0, const at::Tensor& tiles,
-                           const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P, int c_ld, int c_tile0) {
+                           const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P, int c_ld, int c_tile0,
+                           int reserve_cus) {
   check_input(zq_local, "zq_local");
   check_input(zq_chunk, "zq_chunk");
   NTXENT_CHECK(c_ld > 0, "c_ld must be positive");
@@ -418,7 +394,7 @@ at::Tensor coef_gemm_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chun
   const at::DeviceGuard guard(zq_local.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * c_ld * kTileElems}, opts(zq_local, to_scalar(P.bwd())));
   if (n == 0) return cbuf;
-  auto ws = gemm_ws(zq_local, n, P);
+  auto ws = gemm_ws(zq_local, n, P, reserve_cus);
   BlockView bv;
   bv.b_tile0 = b_tile0;
   bv.c_ld = c_ld;
@@ -430,7 +406,7 @@ at::Tensor coef_gemm_tiles(const at::Tensor& zq_local, const at::Tensor& zq_chun
 
 // dZ contribution of one column block: slabs = C_block [rows_pad x rows_pad] * Z_chunk, with
 // zqt_chunk = that rank's [dim_n, ld_t] transposed rows (a one-block, world-1 geometry).
-at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, const Plan& P) {
+at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, const Plan& P, int reserve_cus) {
   check_input(cbuf_block, "cbuf_block");
   check_input(zqt_chunk, "zqt_chunk");
   NTXENT_CHECK(zqt_chunk.numel() == (long)P.g.dim_n * P.g.ld_t, "zqt_chunk must be [dim_n, ld_t]");
@@ -441,7 +417,7 @@ at::Tensor dz_block(const at::Tensor& cbuf_block, const at::Tensor& zqt_chunk, c
   g1.rank = 0;
   g1.col_tiles = g1.row_tiles;
   auto slabs = at::empty({1, P.g.rows_pad, P.g.dim_n}, opts(cbuf_block, at::kFloat));
-  auto ws = gemm_ws(cbuf_block, P.n_dz, P);
+  auto ws = gemm_ws(cbuf_block, P.n_dz, P, reserve_cus);
   launch_dz(P.bwd(), cbuf_block.data_ptr(), zqt_chunk.data_ptr(), reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()),
             P.n_dz, slabs.data_ptr<float>(), ws, g1, cur_stream(cbuf_block));
   return slabs;
@@ -465,7 +441,8 @@ at::Tensor sym_fwd_tiles(const Plan& P, const std::vector<std::tuple<int, int, i
 // Forward tiles `tiles` (own block + kTileCross) over the gathered rows: row partials -> part,
 // column partials of cross tiles -> part_x ([col_tiles, rows_pad, 2], see launch_fwd_stats).
 void fwd_stats_sym(const at::Tensor& zq_local, const at::Tensor& zq_all, const at::Tensor& tiles, const Plan& P,
-                   at::Tensor& part, at::Tensor& part_x, const c10::optional<at::Tensor>& sc, int first, int count) {
+                   at::Tensor& part, at::Tensor& part_x, const c10::optional<at::Tensor>& sc, int first, int count,
+                   int reserve_cus) {
   check_input(zq_local, "zq_local");
   check_input(zq_all, "zq_all");
   check_input(part, "part");
@@ -483,7 +460,7 @@ void fwd_stats_sym(const at::Tensor& zq_local, const at::Tensor& zq_all, const a
                          "sc must hold one tile per entry of `tiles` in the backward dtype");
   if (count == 0) return;
   const at::DeviceGuard guard(zq_local.device());
-  auto ws = gemm_ws(zq_local, count, P);
+  auto ws = gemm_ws(zq_local, count, P, reserve_cus);
   char* scp = keep ? static_cast<char*>(sc->data_ptr()) + (size_t)first * kTileElems * dtype_size(P.bwd()) : nullptr;
   launch_fwd_stats(P.comp, zq_local.data_ptr(), zq_all.data_ptr(), tp + first, count,
                    reinterpret_cast<float2*>(part.data_ptr<float>()), scp, ws, P.g, cur_stream(zq_local), BlockView{},
@@ -520,7 +497,7 @@ void coef_sym(const at::Tensor& sbuf, const at::Tensor& tiles, const at::Tensor&
 // b_block0, column b_col0; a K range longer than one block runs over consecutive whole blocks.
 // `out` is float32 [>= m1 * 256, dim_n] (row tiles may exceed row_tiles: stacked outputs).
 void dz_view(const at::Tensor& abuf, long a_tile0, long a_panel_tiles, const at::Tensor& bbuf, int b_block0, long b_col0,
-             int k_tiles, int m0, int m1, at::Tensor& out, bool accum, const Plan& P) {
+             int k_tiles, int m0, int m1, at::Tensor& out, bool accum, const Plan& P, int reserve_cus) {
   check_input(abuf, "abuf");
   check_input(bbuf, "bbuf");
   check_input(out, "out");
@@ -564,7 +541,7 @@ void dz_view(const at::Tensor& abuf, long a_tile0, long a_panel_tiles, const at:
   const long cs = (long)dtype_size(P.bwd());
   const char* a = static_cast<const char*>(abuf.data_ptr()) + a_tile0 * kTileElems * cs;
   const char* b = static_cast<const char*>(bbuf.data_ptr()) + ((long)b_block0 * blk + b_col0) * cs;
-  auto ws = gemm_ws(abuf, (int)sub.size(0), P);
+  auto ws = gemm_ws(abuf, (int)sub.size(0), P, reserve_cus);
   launch_dz_view(P.bwd(), a, a_panel_tiles, b, kblk_cols, blk, k_tiles, reinterpret_cast<const int4*>(sub.data_ptr<int>()),
                  (int)sub.size(0), out.data_ptr(), accum, ws, P.g, cur_stream(abuf), out_f16);
 }
@@ -641,12 +618,10 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
     return {loss, zq, at::Tensor(), inv, lse2, at::Tensor(), arow};
   }
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
-  // dz_sym plans read Zq itself in the backward (zqt returned EMPTY: the backward's marker).
-  // Otherwise ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes
-  // it from extra blocks beside the merge (one stream: a side-stream transpose cost an event
-  // record and a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
-  const bool sym = P->dz_sym && dz_sym_enabled();
-  auto zqt = sym ? at::empty({0}, pr[0].options()) : at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
+  // ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes it from
+  // extra blocks beside the merge (one stream: a side-stream transpose cost an event record and
+  // a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
+  auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
@@ -671,7 +646,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   }
   // (fp8 plans: 64 spare entries mark the e4m3 forward for the backward, which sees the fp16 rows)
   auto cpos = at::empty({P->g.rows_pad + (f8 ? 64 : 0)}, opts(h, at::kFloat));
-  auto loss = sym ? lse(fs[0], pr[2], lse2, cpos, *P) : lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
+  auto loss = lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
@@ -711,7 +686,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     auto cb = at::empty({(long)P->g.row_tiles * P->g.col_tiles * kTileElems}, opts(h, at::kByte));
     launch_coef(DType::F16, sc_in->data_ptr(), cb.data_ptr(), lse2.data_ptr<float>(), cpos.data_ptr<float>(),
                 reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd, P->g, cur_stream(h), nullptr,
-                false, fuse ? dotp.data_ptr<float>() : nullptr, &q8);
+                fuse ? dotp.data_ptr<float>() : nullptr, &q8);
     NormFuse nf;
     if (fuse) {
       launch_dot_reduce(dotp.data_ptr<float>(), dot.data_ptr<float>(), P->g, cur_stream(h));
@@ -732,12 +707,11 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
                                  cpos.data_ptr<float>());
     return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
   }
-  const bool sym = zqt.numel() == 0;  // dz_sym forward (see fused_forward)
-  // dz_sym plans finish the normalisation backward in the dZ epilogue (norm_fuse_enabled): the
-  // coefficient pass also emits the partials of dot_i = z_i . g_i
+  // 16-bit plans finish the normalisation backward in the dZ epilogue: the coefficient pass also
+  // emits the partials of dot_i = z_i . g_i
   // (not on fp8 plans: the fused dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines)
   const bool f8_fwd = cpos.numel() != P->g.rows_pad;  // see fused_forward
-  const bool fuse = P->bwd() != DType::F32 && !f8_fwd && norm_fuse_enabled() && P->g.dim % 8 == 0;
+  const bool fuse = P->bwd() != DType::F32 && !f8_fwd && P->g.dim % 8 == 0;
   at::Tensor dotp, dot;
   if (fuse) {
     dotp = at::empty({(long)P->g.rows_pad * dot_slots(P->g)}, opts(h, at::kFloat));
@@ -746,7 +720,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   float* dp = fuse ? dotp.data_ptr<float>() : nullptr;
   at::Tensor cb;
   if (sc_in.has_value() && sc_in->defined()) {
-    cb = coef(*sc_in, lse2, cpos, *P, /*upper_only=*/sym, dp);
+    cb = coef(*sc_in, lse2, cpos, *P, dp);
   } else {
     cb = coef_gemm(zq, zq, lse2, cpos, *P, dp);
   }
@@ -764,7 +738,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     nf.dh = dh.data_ptr();
   }
   bool fused = false;
-  auto slabs = sym ? dz_sym(cb, zq, *P, fuse ? &nf : nullptr, &fused) : dz(cb, zqt, *P, fuse ? &nf : nullptr, &fused);
+  auto slabs = dz(cb, zqt, *P, fuse ? &nf : nullptr, &fused);
   return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
 }
 
@@ -840,8 +814,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
   const DType comp = choose_compute(z.scalar_type(), use_mixed_precision, "");
   auto P = get_plan((int)z.size(0), (int)z.size(1), 1, 0, T, dtype_name(comp), z.device().index());
   auto pr = prep(z, *P, c10::nullopt, c10::nullopt);
-  const bool sym = P->dz_sym && dz_sym_enabled();
-  auto zqt = sym ? at::Tensor() : transpose(pr[0], *P, c10::nullopt);
+  auto zqt = transpose(pr[0], *P, c10::nullopt);
   const long R = z.size(0), n = R / 2, Rp = P->g.rows_pad;
   at::Tensor lse2, cpos;
   const bool have_lse = stats.defined() && stats.dim() == 1 && stats.size(0) == R && stats.is_floating_point() &&
@@ -863,7 +836,7 @@ std::tuple<at::Tensor, at::Tensor> backward_op(const at::Tensor& z_in, const at:
     lse(fs[0], pr[2], lse2, cpos, *P);
   }
   auto sc = coef_gemm(pr[0], pr[0], lse2, cpos, *P);
-  auto slabs = sym ? dz_sym(sc, pr[0], *P) : dz(sc, zqt, *P);
+  auto slabs = dz(sc, zqt, *P);
   auto go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
   auto dh = norm_bwd(slabs, z, pr[1], go, *P);
   at::Tensor grad_logits;
@@ -965,19 +938,28 @@ class NativeEngine {
     at::Tensor dh = backward(c10::nullopt);
     return {loss_tensor(), dh};
   }
-  // hipGraph of one step for fixed h (dh is returned and reused by every replay)
+  // hipGraph of one step for fixed h (dh is returned and reused by every replay). The graph
+  // holds h's and dh's device pointers, so both are kept alive in their own members (gh_, gdh_)
+  // for as long as the graph exists, whatever forward()/step() do with h_ in between.
+  // Single process only: a captured step of a multi-rank engine would bake RCCL calls into the
+  // graph.
   at::Tensor capture(const at::Tensor& h) {
     check_h(h);
+    NTXENT_CHECK(world() == 1, "NativeEngine.capture: single-process engines only (world == 1)");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
-    h_ = h;
-    gdh_ = at::empty_like(h);
-    eng_->capture(h.data_ptr(), gdh_.data_ptr(), cur_stream(h));
+    at::Tensor dh = at::empty_like(h);
+    eng_->capture(h.data_ptr(), dh.data_ptr(), cur_stream(h));
+    gh_ = h;
+    gdh_ = dh;
+    h_ = h;  // loss_tensor() after a replay reads the graph's forward
     return gdh_;
   }
   void replay() {
-    NTXENT_CHECK(eng_->captured(), "NativeEngine.replay needs capture()");
+    NTXENT_CHECK(eng_->captured() && gh_.defined(), "NativeEngine.replay needs capture()");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(device_);
-    eng_->replay(cur_stream(h_));
+    // the engine's backward reads the forward input: point it back at the captured one
+    h_ = gh_;
+    eng_->replay(cur_stream(gh_));
   }
   size_t device_bytes() const { return eng_->device_bytes(); }
   bool symmetric() const { return eng_->symmetric(); }
@@ -997,7 +979,8 @@ class NativeEngine {
   at::ScalarType in_ = at::kBFloat16;
   std::unique_ptr<RcclComm> comm_;  // declared before eng_: destroyed after it
   std::unique_ptr<Engine> eng_;
-  at::Tensor h_, gdh_;
+  at::Tensor h_;         // input of the last forward (read by backward)
+  at::Tensor gh_, gdh_;  // the captured graph's input and output (alive while the graph exists)
 };
 }  // namespace
 
@@ -1050,7 +1033,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
       .def_readonly("small", &Plan::small)
-      .def_readonly("dz_sym", &Plan::dz_sym)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
   py::class_<NativeEngine>(m, "NativeEngine")
@@ -1081,66 +1063,42 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("prep", &prep, py::arg("h"), py::arg("plan"), py::arg("zq_out") = py::none(), py::arg("zq8_out") = py::none());
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
-        py::arg("sc"), py::arg("first"), py::arg("count"));
+        py::arg("sc"), py::arg("first"), py::arg("count"), py::arg("reserve_cus") = 0);
   m.def("fwd_stats", [](const at::Tensor& zl, const at::Tensor& za, const Plan& P, bool keep) {
     return fwd_stats(zl, za, P, keep, true);
   }, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("keep_cos"));
   m.def("lse", &lse, py::arg("part"), py::arg("ypos"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
         py::arg("zq") = py::none(), py::arg("zqt") = py::none());
-  m.def("coef", [](const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
-                   bool upper_only) { return coef(sbuf, lse2_all, cpos, P, upper_only); },
-        py::arg("sbuf"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("upper_only") = false);
+  m.def("coef", [](const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P) {
+    return coef(sbuf, lse2_all, cpos, P);
+  }, py::arg("sbuf"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"));
   m.def("coef_gemm", [](const at::Tensor& zl, const at::Tensor& za, const at::Tensor& lse2_all, const at::Tensor& cpos,
                         const Plan& P) { return coef_gemm(zl, za, lse2_all, cpos, P); });
   m.def("dz", [](const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) { return dz(sc, zqt_all, P); });
-  m.def("dz_sym", [](const at::Tensor& cbuf, const at::Tensor& zq_all, const Plan& P) { return dz_sym(cbuf, zq_all, P); },
-        py::arg("cbuf"), py::arg("zq_all"), py::arg("plan"));
-  m.def("set_dz_sym", &ntxent::set_dz_sym, py::arg("on"));
-  m.def("set_norm_fuse", &ntxent::set_norm_fuse, py::arg("on"));
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
-  m.def("set_fwd_stream", &ntxent::set_fwd_stream, py::arg("on"));
-  m.def("fwd_stream_enabled", &ntxent::fwd_stream_enabled);
-  m.def("set_splitk_piece_major", &ntxent::set_splitk_piece_major, py::arg("on"));
-  m.def("splitk_piece_major", &ntxent::splitk_piece_major);
-  m.def("set_splitk_half", &ntxent::set_splitk_half, py::arg("on"));
-  m.def("splitk_half", &ntxent::splitk_half);
-  m.def("set_splitk_dz_half", &ntxent::set_splitk_dz_half, py::arg("on"));
-  m.def("splitk_dz_half", &ntxent::splitk_dz_half);
-  m.def("set_diag_upper", &ntxent::set_diag_upper, py::arg("on"));
-  m.def("diag_upper_enabled", &ntxent::diag_upper_enabled);
-  m.def("set_superblock_order", &ntxent::set_superblock_order, py::arg("on"));
-  m.def("superblock_order_enabled", &ntxent::superblock_order_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
-  m.def("norm_fuse_enabled", &ntxent::norm_fuse_enabled);
-  m.def("dz_sym_enabled", &ntxent::dz_sym_enabled);
-  m.def("set_diag_strips", &ntxent::set_diag_strips, py::arg("on"));
-  m.def("set_splitk_reduce", &ntxent::set_splitk_reduce, py::arg("on"));
-  m.def("set_diag_subtiles", &ntxent::set_diag_subtiles, py::arg("on"));
-  m.def("splitk_reduce_enabled", &ntxent::splitk_reduce_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
-  m.def("diag_strips_enabled", &ntxent::diag_strips_enabled);
   m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"));
   m.def("fwd_stats_tiles", &fwd_stats_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
-        py::arg("tiles"), py::arg("plan"), py::arg("part"));
+        py::arg("tiles"), py::arg("plan"), py::arg("part"), py::arg("reserve_cus") = 0);
   m.def("coef_gemm_tiles", &coef_gemm_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
-        py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("c_ld"), py::arg("c_tile0"));
-  m.def("dz_block", &dz_block, py::arg("cbuf_block"), py::arg("zqt_chunk"), py::arg("plan"));
+        py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"), py::arg("c_ld"), py::arg("c_tile0"),
+        py::arg("reserve_cus") = 0);
+  m.def("dz_block", &dz_block, py::arg("cbuf_block"), py::arg("zqt_chunk"), py::arg("plan"), py::arg("reserve_cus") = 0);
   m.def("sym_fwd_tiles", &sym_fwd_tiles, py::arg("plan"), py::arg("jobs"), py::arg("nchunks") = 1);
   m.def("fwd_stats_sym", &fwd_stats_sym, py::arg("zq_local"), py::arg("zq_all"), py::arg("tiles"), py::arg("plan"),
-        py::arg("part"), py::arg("part_x"), py::arg("sc"), py::arg("first"), py::arg("count"));
+        py::arg("part"), py::arg("part_x"), py::arg("sc"), py::arg("first"), py::arg("count"), py::arg("reserve_cus") = 0);
   m.def("coef_sym", &coef_sym, py::arg("sbuf"), py::arg("tiles"), py::arg("lse2_all"), py::arg("cpos"), py::arg("plan"),
         py::arg("cbuf"), py::arg("mbuf"));
   m.def("dz_view", &dz_view, py::arg("abuf"), py::arg("a_tile0"), py::arg("a_panel_tiles"), py::arg("bbuf"),
         py::arg("b_block0"), py::arg("b_col0"), py::arg("k_tiles"), py::arg("m0"), py::arg("m1"), py::arg("out"),
-        py::arg("accum"), py::arg("plan"));
+        py::arg("accum"), py::arg("plan"), py::arg("reserve_cus") = 0);
   m.def("norm_bwd_slabs", &norm_bwd_slabs, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"),
         py::arg("plan"), py::arg("xslabs") = py::none());
   m.def("fused_forward", &fused_forward, py::arg("h"), py::arg("T"), py::arg("compute") = "auto",
         py::arg("keep_cos") = true);
   m.def("fused_backward", &fused_backward);
-  m.def("set_grid_reserve", &ntxent::set_grid_reserve, py::arg("cus"),
-        "CUs the next similarity-GEMM launches leave free (for overlapped RCCL kernels); returns the old value");
   m.def("set_small_path", &ntxent::set_small_path, py::arg("on"));
   m.def("small_path_enabled", &ntxent::small_path_enabled);
   m.def("set_small_splits", &ntxent::set_small_splits, py::arg("n"));

@@ -120,8 +120,13 @@ class SimCLRTrainer:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
+        # Data-parallel steps run on their own (high-priority) stream, entered per step: the RCCL
+        # kernels of overlapped transfers then do not share the compute stream's hardware queue
+        # (commstats.use_compute_stream). Kept on self and entered in train_step(), so the caller's
+        # current stream is never switched; each step is ordered after the caller's queued work.
+        self.stream = None
         if device.type == "cuda" and cfg.compute_stream != "default":
-            torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=-1 if cfg.compute_stream == "high" else 0))
+            self.stream = torch.cuda.Stream(device=device, priority=-1 if cfg.compute_stream == "high" else 0)
         torch.manual_seed(cfg.seed)
         model = build_model(cfg).to(device)
         if device.type == "cuda":
@@ -148,6 +153,16 @@ class SimCLRTrainer:
                 self.step = st["step"]
 
     def train_step(self) -> Dict:
+        if self.stream is None:
+            return self._train_step()
+        caller = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            rec = self._train_step()
+        caller.wait_stream(self.stream)
+        return rec
+
+    def _train_step(self) -> Dict:
         cfg = self.cfg
         for g, base in zip(self.opt.param_groups, self.base_lrs):
             g["lr"] = lr_at(self.step, cfg, base)

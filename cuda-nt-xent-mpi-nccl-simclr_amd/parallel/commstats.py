@@ -69,28 +69,14 @@ def comm_reserve_cus(backend: str = "nccl") -> int:
     the whole register file), so without a reserve the RCCL kernels of an overlapped P2P /
     all-gather cannot be scheduled until the GEMM ends. ``NTXENT_COMM_RESERVE_CUS`` overrides
     the default of 8 (one per XCD: 3 % of the chip); gloo transfers are host-staged and complete
-    before the GEMM is launched, so they reserve nothing."""
+    before the GEMM is launched, so they reserve nothing. The value is passed per launch
+    (``reserve_cus=`` of the stage ops): no process-wide state, so GEMMs on concurrent streams
+    each keep their own reserve."""
     if backend == "gloo":
         return 0
     import os
 
     return max(0, int(os.environ.get("NTXENT_COMM_RESERVE_CUS", "8")))
-
-
-@contextlib.contextmanager
-def comm_overlap(cus: int):
-    """GEMMs launched inside the block leave ``cus`` CUs free (see :func:`comm_reserve_cus`)."""
-    if cus <= 0:
-        yield
-        return
-    from ..ops import _ext
-
-    C = _ext.load()
-    old = C.set_grid_reserve(int(cus))
-    try:
-        yield
-    finally:
-        C.set_grid_reserve(old)
 
 
 def rccl_shared_gpu_env(rank: int) -> Dict[str, str]:

@@ -25,7 +25,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
-from .commstats import comm_overlap, comm_reserve_cus, span
+from .commstats import comm_reserve_cus, span
 
 
 def _world(group) -> tuple[int, int]:
@@ -102,13 +102,13 @@ class DistNTXentFunction(torch.autograd.Function):
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=h.device)
         sc = torch.empty((plan.n_fwd_tiles * 256 * 256,), dtype=cdt, device=h.device) if keep_logits else None
         # own-rank (upper-triangular) tiles need only this rank's slot: they overlap the gather
-        with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if W > 1 else 0):
-            C.fwd_stats_range(fwd, fwd_all, plan, part, sc, 0, plan.n_own_tiles)
+        reserve = comm_reserve_cus(dist.get_backend(group)) if W > 1 else 0
+        C.fwd_stats_range(fwd, fwd_all, plan, part, sc, 0, plan.n_own_tiles, reserve_cus=reserve)
         if work_z is not None:
             with span("fwd_rows"):
                 work_z.wait()
-        with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if work_t is not None else 0):  # ZqT gather
-            C.fwd_stats_range(fwd, fwd_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles)
+        C.fwd_stats_range(fwd, fwd_all, plan, part, sc, plan.n_own_tiles, plan.n_fwd_tiles - plan.n_own_tiles,
+                          reserve_cus=reserve if work_t is not None else 0)  # the ZqT gather is in flight
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)

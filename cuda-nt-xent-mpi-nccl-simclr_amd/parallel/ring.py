@@ -29,7 +29,7 @@ import torch.distributed as dist
 
 from ..ops import _ext
 from ..ops.ntxent import resolve_compute
-from .commstats import comm_overlap, comm_reserve_cus, span
+from .commstats import comm_reserve_cus, span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 _TILE_CACHE: Dict[tuple, Dict[int, torch.Tensor]] = {}
@@ -73,7 +73,8 @@ def _exchange(send: torch.Tensor, recv: torch.Tensor, group):
 
 
 def _ring(zq: torch.Tensor, group, fn):
-    """Calls fn(q, rows_of_q) for q = r, r-1, ..., r-W+1 while the next block travels."""
+    """Calls fn(q, rows_of_q, reserve_cus) for q = r, r-1, ..., r-W+1 while the next block
+    travels; reserve_cus = the CUs its GEMMs leave free for the transfer in flight."""
     W, r = _world(group)
     bufs = [torch.empty_like(zq), torch.empty_like(zq)] if W > 1 else []
     cur = zq
@@ -84,8 +85,7 @@ def _ring(zq: torch.Tensor, group, fn):
         if s < W - 1:
             nxt = bufs[s % 2]
             works = _exchange(cur, nxt, group)
-        with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if works else 0):
-            fn(q, cur)
+        fn(q, cur, comm_reserve_cus(dist.get_backend(group)) if works else 0)
         with span("ring_rows"):
             for w in works:
                 w.wait()
@@ -107,7 +107,7 @@ class RingNTXentFunction(torch.autograd.Function):
         zq, inv, ypos, _ = C.prep(h, plan)
         tiles = block_tiles(C, plan, h.device)
         part = torch.empty((plan.col_tiles, Rpad, 2), dtype=torch.float32, device=h.device)
-        _ring(zq, group, lambda q, rows: C.fwd_stats_tiles(zq, rows, q * rt, tiles[q], plan, part))
+        _ring(zq, group, lambda q, rows, res: C.fwd_stats_tiles(zq, rows, q * rt, tiles[q], plan, part, reserve_cus=res))
         lse2_all = torch.empty((W * Rpad,), dtype=torch.float32, device=h.device)
         cpos = torch.empty((Rpad,), dtype=torch.float32, device=h.device)
         loss = C.lse(part, ypos, lse2_all, cpos, plan)
@@ -129,9 +129,9 @@ class RingNTXentFunction(torch.autograd.Function):
         tiles = block_tiles(C, plan, h.device)
         acc: List[Optional[torch.Tensor]] = [None]
 
-        def block(q, rows):
-            cb = C.coef_gemm_tiles(zq, rows, q * rt, tiles[q], lse2_all, cpos, plan, rt, q * rt)
-            slabs = C.dz_block(cb, C.transpose(rows, plan), plan)
+        def block(q, rows, res):
+            cb = C.coef_gemm_tiles(zq, rows, q * rt, tiles[q], lse2_all, cpos, plan, rt, q * rt, reserve_cus=res)
+            slabs = C.dz_block(cb, C.transpose(rows, plan), plan, reserve_cus=res)
             acc[0] = slabs if acc[0] is None else acc[0].add_(slabs)
 
         _ring(zq, group, block)

@@ -40,7 +40,7 @@ import torch.distributed as dist
 
 from ..ops import _ext, reference
 from ..ops.ntxent import resolve_compute
-from .commstats import comm_overlap, comm_reserve_cus, span
+from .commstats import comm_reserve_cus, span
 from .distributed import _all_gather_into, _is_gloo, _world
 
 Job = Tuple[int, int, int, int, int]  # (q, m0, m1, k0, k1): my row tiles [m0,m1) x q's row tiles [k0,k1)
@@ -200,8 +200,8 @@ class SymNTXentFunction(torch.autograd.Function):
         part_x = torch.empty_like(part)
         sc = torch.empty((ntiles * 256 * 256,), dtype=cdt, device=dev)
         reserve = comm_reserve_cus(dist.get_backend(group))
-        with comm_overlap(reserve):  # chunk 0 of the rows is on the wire
-            C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles)
+        # chunk 0 of the rows is on the wire
+        C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, 0, plan.n_own_tiles, reserve_cus=reserve)
         segs = sym_chunk_segments(plan, jobs, nch)
         for c, (ws, (first, count)) in enumerate(zip(works, segs)):
             with span("fwd_rows"):
@@ -209,8 +209,8 @@ class SymNTXentFunction(torch.autograd.Function):
                     w.wait()
             # the next chunk (or the fp16 rows of an fp8 plan) is still on the wire
             more = c + 1 < len(works) and bool(works[c + 1]) or bool(works_f16)
-            with comm_overlap(reserve if more else 0):
-                C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count)
+            C.fwd_stats_sym(fwd, fwd_all, tiles, plan, part, part_x, sc, first, count,
+                            reserve_cus=reserve if more else 0)
         with span("fwd_rows"):
             for w in works_f16:
                 w.wait()
@@ -329,20 +329,21 @@ def sym_norm_bwd(C, plan, own, recv, h, inv, grad_out):
     return C.norm_bwd_slabs(own, h, inv, grad_out.reshape(1), plan, recv)
 
 
-def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out):
+def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out, reserve_cus=0):
     """This rank's own contributions into ``out`` [Rpad, dim_n]: C_{r,r} Z_r + the full blocks
     C_{r,q} Z_q (one GEMM over the consecutive rank blocks r..r+nfull, two if they wrap) + the
-    split block's rows."""
+    split block's rows. The GEMMs leave ``reserve_cus`` CUs free for transfers in flight."""
     rt, ct = plan.row_tiles, plan.col_tiles
     full, split = _split_jobs(sym_jobs(W, r, rt), rt)
     nb = 1 + len(full)  # blocks r, r+1, ..., r+nfull (mod W)
     first = min(nb, W - r)
-    C.dz_view(cbuf, r * rt, ct, zqt_all, r, 0, first * rt, 0, rt, out, False, plan)
+    C.dz_view(cbuf, r * rt, ct, zqt_all, r, 0, first * rt, 0, rt, out, False, plan, reserve_cus=reserve_cus)
     if nb > first:
-        C.dz_view(cbuf, 0, ct, zqt_all, 0, 0, (nb - first) * rt, 0, rt, out, True, plan)
+        C.dz_view(cbuf, 0, ct, zqt_all, 0, 0, (nb - first) * rt, 0, rt, out, True, plan, reserve_cus=reserve_cus)
     if split is not None:
         q, m0, m1, k0, k1 = split
-        C.dz_view(cbuf, q * rt + k0, ct, zqt_all, q, k0 * 256, k1 - k0, m0, m1, out, True, plan)
+        C.dz_view(cbuf, q * rt + k0, ct, zqt_all, q, k0 * 256, k1 - k0, m0, m1, out, True, plan,
+                  reserve_cus=reserve_cus)
 
 
 def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc, grad_out, group):
@@ -354,8 +355,7 @@ def sym_backward_local(C, plan, W, r, h, inv, zqt_all, lse2_all, cpos, tiles, sc
     contrib = sym_partner_grads(C, plan, W, r, mbuf, zqt_all)
     own, recv, views = sym_grad_slabs(plan, W, r, h.device)
     works = _p2p([(t, q) for q, t in contrib.items()], [(v, p) for p, v in views.items()], group)
-    with comm_overlap(comm_reserve_cus(dist.get_backend(group)) if works else 0):
-        sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0])
+    sym_own_grad(C, plan, W, r, cbuf, zqt_all, own[0], comm_reserve_cus(dist.get_backend(group)) if works else 0)
     with span("bwd_partner_grads"):
         for w in works:
             w.wait()

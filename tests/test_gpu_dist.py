@@ -67,15 +67,17 @@ def _large_path():
 
     mod = _ext.load(build_if_missing=False)
     mod.set_small_path(False)
-    # (and the unfused normalisation backward: the emulated ranks run the data-parallel stage
-    # ops, whose dZ slab goes through launch_norm_bwd)
-    old_fuse = mod.norm_fuse_enabled()
-    mod.set_norm_fuse(False)
     try:
         yield
     finally:
         mod.set_small_path(True)
-        mod.set_norm_fuse(old_fuse)
+
+
+def _close_grad(g, g2, rel=2e-3):
+    """The data-parallel stage ops finish the normalisation backward in launch_norm_bwd (dot from
+    the fp16 dZ slab); the single-GPU large path fuses it into the dZ epilogue (dot from the
+    coefficient pass): equal up to the rounding of the two dot products."""
+    assert (g.float() - g2.float()).abs().max().item() <= rel * g2.float().abs().max().item()
 
 
 def test_emulated_world1_equals_single_gpu():
@@ -84,13 +86,14 @@ def test_emulated_world1_equals_single_gpu():
 
     h = _shards(1, 300, 96, seed=5)[0].float().cuda()
     loss, (g,) = emulated_dist_forward_backward([h], 0.07, compute="fp16")
-    # the emulated ranks run the large-problem pipeline: bitwise equal to it at world 1
+    # the emulated ranks run the large-problem pipeline: the same forward at world 1 (bitwise
+    # loss), the gradient up to the normalisation backward's rounding (_close_grad)
     with _large_path():
         x = h.clone().requires_grad_(True)
         l2 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
         (g2,) = torch.autograd.grad(l2, x)
     assert loss.item() == l2.item()
-    assert torch.equal(g, g2)
+    _close_grad(g, g2)
     # ... and within rounding of the single-launch small-problem path this shape selects
     x = h.clone().requires_grad_(True)
     l3 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
@@ -135,7 +138,7 @@ def test_rccl_path_world1(nccl_world1, overlap):
         l2 = ntxent_amd.ntxent_loss(y, 0.07)
         (g2,) = torch.autograd.grad(l2, y)
     assert loss.item() == l2.item()
-    assert torch.equal(g, g2)
+    _close_grad(g, g2)
 
 
 def test_rccl_reduce_scatter_backward_world1(nccl_world1):

@@ -61,6 +61,36 @@ def test_native_engine_graph_replay_matches_step():
     assert gl.item() == loss.item()
 
 
+def test_native_engine_graph_keeps_captured_input_alive():
+    """The graph holds the captured h's device pointer: the engine keeps that tensor alive itself,
+    so capture(h); del h; step(h2); replay() still replays the captured step (no read of freed
+    memory), and a multi-rank capture is refused."""
+    from ntxent_amd.parallel.native import NativeNTXent
+
+    rows, dim = 4096, 256
+    eng = NativeNTXent(rows, dim, 0.1)
+    h = _h(rows, dim, 5)
+    ref_loss, ref_dh = eng.step(h)
+    ref_loss, ref_dh = ref_loss.clone(), ref_dh.clone()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        gdh = eng.capture(h.clone())  # the only reference to the captured input is the engine's
+    side.synchronize()
+    del h
+    # an eager step on other data in between (it overwrites the engine's forward input h_)
+    h2 = _h(rows, dim, 6)
+    l2, _ = eng.step(h2)
+    torch.cuda.synchronize()
+    # churn the caching allocator so a freed captured input would be reused and overwritten
+    junk = [torch.full((rows, dim), 7.0, dtype=torch.bfloat16, device="cuda") for _ in range(4)]
+    with torch.cuda.stream(side):
+        gl = eng.replay()
+    side.synchronize()
+    del junk
+    assert gl.item() == ref_loss.item() and gl.item() != l2.item()
+    assert torch.equal(gdh, ref_dh)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -6,8 +6,8 @@ branches with a world-1 NCCL process group instead:
 
   * ``_p2p``'s ``dist.batch_isend_irecv`` branch (self send/recv in one grouped batch: RCCL
     runs it as a device kernel on the communicator's stream, like a peer transfer);
-  * ``comm_overlap`` with the RCCL CU reserve (the GEMM leaves CUs free while a transfer is in
-    flight) -- results must be bitwise those of the un-overlapped launch;
+  * the RCCL CU reserve (``reserve_cus``: the GEMM leaves CUs free while a transfer is in
+    flight) -- results must be bitwise those of the same launch without the transfer;
   * the all-gather / ring / symmetric data-parallel autograd functions end to end on RCCL
     collectives (world 1: every collective is a device-local copy), against the single-GPU op.
 """
@@ -75,7 +75,7 @@ def test_comm_overlap_reserve_is_bitwise_neutral(nccl_group, ext):
     flight gives exactly the results of the same launch without the transfer (the reserve
     changes the persistent schedule, hence the rounding of split tiles: against the unreserved
     launch it is held to rounding level)."""
-    from ntxent_amd.parallel.commstats import comm_overlap, comm_reserve_cus
+    from ntxent_amd.parallel.commstats import comm_reserve_cus
     from ntxent_amd.parallel.symmetric import _p2p
 
     reserve = comm_reserve_cus("nccl")
@@ -89,12 +89,12 @@ def test_comm_overlap_reserve_is_bitwise_neutral(nccl_group, ext):
         big = torch.ones(64 * 1024 * 1024, dtype=torch.float32, device="cuda")
         dst = torch.empty_like(big)
         works = _p2p([(big, 0)], [(dst, 0)], nccl_group) if xfer else []
-        with comm_overlap(res):
-            part, sc = ext.fwd_stats(zq, zq, plan, True)
+        part = torch.empty((plan.col_tiles, plan.rows_pad, 2), dtype=torch.float32, device="cuda")
+        sc = torch.zeros((plan.n_fwd_tiles * 256 * 256,), dtype=torch.float16, device="cuda")
+        ext.fwd_stats_range(zq, zq, plan, part, sc, 0, plan.n_fwd_tiles, reserve_cus=res)
         for w in works:
             w.wait()
         torch.cuda.synchronize()
-        assert ext.set_grid_reserve(0) == 0  # restored by the context manager
         outs[(res, xfer)] = (part.clone(), sc.clone())
         if xfer:
             assert torch.equal(dst, big)

@@ -3,7 +3,7 @@
 
 A world-1 RCCL process group runs a self send/recv batch (one grouped P2P, executed by an RCCL
 device kernel on the communicator's stream, like a peer transfer over xGMI) while the forward
-similarity GEMM runs on the compute stream under ``set_grid_reserve(n)``. The persistent GEMM
+similarity GEMM runs on the compute stream with ``reserve_cus=n``. The persistent GEMM
 holds every CU it is given for its whole duration (128 KiB LDS, the full register file), so
 with n = 0 the RCCL kernel can only start when the GEMM ends; with n > 0 it runs on the
 reserved CUs underneath the GEMM. For each n this prints the GEMM alone, the transfer alone,
@@ -69,8 +69,11 @@ def main():
     torch.cuda.set_stream(comp)
     print(f"GPU_MAX_HW_QUEUES={os.environ.get('GPU_MAX_HW_QUEUES')} gemm stream={a.gemm_stream}", flush=True)
 
+    reserve = [0]
+    part = torch.empty((plan.col_tiles, plan.rows_pad, 2), dtype=torch.float32, device="cuda")
+
     def gemm():
-        C.fwd_stats(zq, zq, plan, True)
+        C.fwd_stats_range(zq, zq, plan, part, None, 0, plan.n_fwd_tiles, reserve_cus=reserve[0])
 
     def xfer():
         return _p2p([(t, 0) for t in src], [(t, 0) for t in dst], dist.group.WORLD)
@@ -93,11 +96,10 @@ def main():
     for _ in range(3):  # warm-up (plans, communicator, clocks)
         timed(gemm, xfer)
     for r in [int(x) for x in a.reserves.split(",")]:
-        old = C.set_grid_reserve(r)
+        reserve[0] = r
         g_us = statistics.median(timed(gemm, None) for _ in range(a.iters))
         x_us = statistics.median(timed(None, xfer) for _ in range(a.iters))
         b_us = statistics.median(timed(gemm, xfer) for _ in range(a.iters))
-        C.set_grid_reserve(old)
         hidden = (g_us + x_us - b_us) / x_us if x_us > 0 else 0.0
         rec = {"reserve_cus": r, "gemm_us": round(g_us, 1), "xfer_us": round(x_us, 1), "both_us": round(b_us, 1),
                "xfer_hidden_frac": round(hidden, 3)}
