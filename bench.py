@@ -101,16 +101,28 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def rank_env(base: dict, r: int, n: int, port: int) -> dict:
+    """Environment of rank r of an n-rank single-node job (what torchrun would set): rank r is
+    LOCAL_RANK r, so run_rank puts it on cuda:r (rank_device)."""
+    env = dict(base)
+    env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **{CHILD_ENV: "1"})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return env
+
+
+def rank_device(local_rank: int, share_gpu: bool) -> int:
+    """GPU index of a rank: its LOCAL_RANK (one rank per GPU), or 0 for the one-GPU rehearsal."""
+    return 0 if share_gpu else int(local_rank)
+
+
 def launch(a, argv) -> int:
     """Start a.gpus rank processes of this script and relay rank 0's JSON line."""
     n = a.gpus
     port = _free_port()
     procs = []
     for r in range(n):
-        env = dict(os.environ)
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **{CHILD_ENV: "1"})
-        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+        env = rank_env(os.environ, r, n, port)
         cmd = [sys.executable, "-u", str(Path(__file__).resolve()), *argv]
         # rank 0's stdout carries the JSON line; every rank's stderr passes through
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
@@ -190,7 +202,9 @@ def run_rank(a) -> None:
     if not on_gpu and backend != "gloo":
         raise SystemExit("--device cpu needs the gloo backend")
     if on_gpu:
-        dev_index = 0 if a.share_gpu else local_rank
+        dev_index = rank_device(local_rank, a.share_gpu)
+        if not a.share_gpu and dev_index >= torch.cuda.device_count():
+            raise SystemExit(f"bench: LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs visible")
         torch.cuda.set_device(dev_index)
         dev = torch.device("cuda", dev_index)
     else:

@@ -524,11 +524,12 @@ NT_TEST(ThreadCommPrimitives) {  // world 1 semantics of the in-process communic
 }
 
 NT_TEST(MultiRankSymmetric) {
-  for (int W : {2, 3, 4}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kSymmetric, 2e-3, 2e-2);
+  // W = 8: the driver's scaling-run world size (3 full partner blocks + a split pair per rank)
+  for (int W : {2, 3, 4, 8}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kSymmetric, 2e-3, 2e-2);
 }
 
 NT_TEST(MultiRankAllGather) {
-  for (int W : {2, 3}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kAllGather, 2e-3, 2e-2);
+  for (int W : {2, 3, 8}) multi_rank_case(W, 512, 128, DType::F16, Negatives::kAllGather, 2e-3, 2e-2);
 }
 
 NT_TEST(MultiRankSymmetricFp32) {  // fp32 contributions on the wire, one slab stack

@@ -77,3 +77,27 @@ def test_scaling_driver_cpu():
     assert c1["samples_efficiency"] == pytest.approx(1.0) and c1["pair_efficiency"] == pytest.approx(1.0)
     assert c2["pair_efficiency"] == pytest.approx(2 * c2["samples_efficiency"], rel=1e-3)  # JSON rounding
     assert doc["runs"]["2"]["n_gpus"] == 2
+
+
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_rank_env_maps_rank_r_to_cuda_r(n):
+    """The driver's scaling run at N = 8: the launcher gives rank r LOCAL_RANK r (and the
+    torchrun-style variables), and a rank places itself on cuda:LOCAL_RANK — one rank per GPU,
+    every GPU used once; the one-GPU rehearsal (--share-gpu) puts every rank on cuda:0. The
+    process group is initialised with device_id = that device (bench.py run_rank)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    envs = [bench.rank_env({"PATH": "/bin"}, r, n, 29500) for r in range(n)]
+    assert [e["RANK"] for e in envs] == [str(r) for r in range(n)]
+    assert [e["LOCAL_RANK"] for e in envs] == [str(r) for r in range(n)]
+    assert all(e["WORLD_SIZE"] == str(n) and e["LOCAL_WORLD_SIZE"] == str(n) for e in envs)
+    assert all(e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29500" for e in envs)
+    assert all(e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e[bench.CHILD_ENV] == "1" for e in envs)
+    devs = [bench.rank_device(int(e["LOCAL_RANK"]), share_gpu=False) for e in envs]
+    assert devs == list(range(n))
+    assert {bench.rank_device(int(e["LOCAL_RANK"]), share_gpu=True) for e in envs} == {0}
+    # the GPU rank path initialises RCCL with the rank's own device (no implicit device 0)
+    src = (ROOT / "bench.py").read_text()
+    assert 'dist.init_process_group("nccl", device_id=dev' in src
+    assert "dev_index = rank_device(local_rank, a.share_gpu)" in src

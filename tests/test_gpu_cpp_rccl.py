@@ -11,7 +11,8 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 
-@pytest.mark.parametrize("W,negatives", [(2, "symmetric"), (2, "allgather"), (3, "symmetric")])
+@pytest.mark.parametrize("W,negatives", [(2, "symmetric"), (2, "allgather"), (3, "symmetric"),
+                                        (8, "symmetric"), (8, "allgather")])  # W = 8: the scaling run
 def test_native_rccl_processes_match_emulated(W, negatives):
     bench = ROOT / "build" / "bin" / "ntxent_bench"
     assert bench.exists(), "build/bin/ntxent_bench missing: run tools/build_ext.py"

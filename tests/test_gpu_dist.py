@@ -73,10 +73,11 @@ def _large_path():
         mod.set_small_path(True)
 
 
-def _close_grad(g, g2, rel=2e-3):
+def _close_grad(g, g2, rel=1e-2):
     """The data-parallel stage ops finish the normalisation backward in launch_norm_bwd (dot from
     the fp16 dZ slab); the single-GPU large path fuses it into the dZ epilogue (dot from the
-    coefficient pass): equal up to the rounding of the two dot products."""
+    coefficient pass): equal up to the rounding of the two dot products (a bf16 output ulp is
+    ~4e-3 of max|g|)."""
     assert (g.float() - g2.float()).abs().max().item() <= rel * g2.float().abs().max().item()
 
 

@@ -72,6 +72,7 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives
     (4, 256, 64, "fp32", True, True, "symmetric", "symmetric"),
     (3, 384, 80, "fp16", True, True, "symmetric", "symmetric"),
     (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric"),  # 16 row tiles: 4 exchange chunks
+    (8, 128, 64, "fp32", False, True, "symmetric", "ring"),        # W = 8 ring
 ])
 def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
     _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "gloo")
@@ -89,6 +90,10 @@ def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, ne
     (2, 300, 96, "fp16", False, True, "symmetric", "allgather"),
     (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather"),
     (2, 256, 128, "fp16", False, True, "symmetric", "ring"),
+    # W = 8, the driver's scaling-run world size: 3 full partner blocks + a split pair per rank
+    # (symmetric), 7 gathered blocks (all-gather); 8 processes sharing the GPU over sockets
+    (8, 256, 64, "fp16", True, True, "symmetric", "symmetric"),
+    (8, 256, 64, "fp16", False, True, "symmetric", "allgather"),
 ])
 def test_multiprocess_rccl_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
     _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "nccl")
