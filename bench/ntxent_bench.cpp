@@ -171,6 +171,35 @@ class Bench {
 
   void fwd() { e_->forward(h_, s_); }
   void bwd() { e_->backward(nullptr, dh_, s_); }
+  // Bit pattern checksum of dh after one fwd + bwd (FNV-1a over the raw bytes) plus its L1 norm:
+  // two builds whose kernels differ only in data layout or prefetching must print the same hash.
+  std::pair<unsigned long long, double> grad_digest() {
+    fwd();
+    bwd();
+    NTXENT_HIP_CHECK(hipStreamSynchronize(s_));
+    const size_t n = host_.size(), es = dtype_size(in_);
+    std::vector<unsigned char> raw(n * es);
+    NTXENT_HIP_CHECK(hipMemcpy(raw.data(), dh_, raw.size(), hipMemcpyDeviceToHost));
+    unsigned long long hsh = 1469598103934665603ull;
+    for (unsigned char c : raw) hsh = (hsh ^ c) * 1099511628211ull;
+    double l1 = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      float v;
+      if (es == 4) std::memcpy(&v, &raw[4 * i], 4);
+      else {
+        unsigned short u;
+        std::memcpy(&u, &raw[2 * i], 2);
+        if (in_ == DType::BF16) {
+          const unsigned w = (unsigned)u << 16;
+          std::memcpy(&v, &w, 4);
+        } else {
+          v = (float)*reinterpret_cast<const _Float16*>(&u);
+        }
+      }
+      l1 += std::fabs((double)v);
+    }
+    return {hsh, l1};
+  }
 
   // times `which` (0 fwd, 1 bwd, 2 fwd+bwd, 3 fwd+bwd as one hipGraph) with hipEvents
   std::vector<float> time(int which, int warmup, int iters) {
@@ -263,7 +292,7 @@ struct Options {
   int batch = 0, dim = 0, iters = 100, warmup = 1, gpus = 1;
   std::string dtype = "bf16", compute = "auto", json;
   float T = 0.07f;
-  bool check = false, graph = false, recompute = false, small = true;
+  bool check = false, graph = false, recompute = false, small = true, grad_digest = false;
   int small_splits = 0;
   Negatives negatives = Negatives::kSymmetric;
   bool emulate = false;  // --gpus N as N emulated ranks on GPU 0 (ThreadComm), not N GPUs over RCCL
@@ -390,6 +419,7 @@ int main(int argc, char** argv) {
     else if (a == "--gpus") o.gpus = std::stoi(next());
     else if (a == "--json") o.json = next();
     else if (a == "--check") o.check = true;
+    else if (a == "--grad-digest") o.grad_digest = true;
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
     else if (a == "--no-small") o.small = false;
@@ -416,6 +446,7 @@ int main(int argc, char** argv) {
                   "  --gpus N --proc-rank r --uid-file F [--shared-gpu]: rank r of N processes over RCCL\n"
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
+                  "  --grad-digest: print a hash of dh after one step (build variants must match bitwise)\n"
                   "  (the measured A/B alternatives of earlier rounds are deleted; build-time variants:\n"
                   "   tools/build_variant.sh)\n");
       return 0;
@@ -468,6 +499,10 @@ int main(int argc, char** argv) {
                    bw.mx, fb.mean, fb.stdev, fb.mn, fb.mx, gr.mean, b / (best * 1e-3), tf,
                    bench.engine().device_bytes());
       first = false;
+    }
+    if (o.grad_digest) {
+      const auto gd = bench.grad_digest();
+      std::printf("       grad digest: %016llx l1 %.9e loss %.6f\n", gd.first, gd.second, bench.loss());
     }
     if (o.check && b <= 1024 && d <= 512) {
       bench.fwd();

@@ -788,6 +788,26 @@ int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipSt
 // elements get 64 extra so the rows a tile streams rotate through the L2 channels.
 int padded_ld(int n) { return (n % 1024 == 0) ? n + 64 : n; }
 
+// The coefficient tiles as the dZ GEMM's A operand: tile (I, J) of a row panel of `panel_tiles`
+// tiles; 256 K-columns per tile. Row-major tiles: rows of 256 elements, every 256 K-columns jump
+// to the next tile of the panel. K-step-blocked tiles (NTXENT_C_KB, dev::ctile_off): a K-step of
+// a row panel is one 32 KiB block [256 rows][128 B] and the K-steps of a panel follow each other.
+dev::OperandDesc coef_tile_operand(const void* base, long long panel_tiles, long long cs) {
+  dev::OperandDesc o;
+  o.base = static_cast<const char*>(base);
+  o.row_tile_stride = panel_tiles * kTileElems * cs;
+  if (NTXENT_C_KB) {
+    o.ld = kKStepBytes;
+    o.kblk = kKStepBytes;
+    o.kblk_stride = (long long)kTile * kKStepBytes;
+  } else {
+    o.ld = kTile * cs;
+    o.kblk = kTile * cs;
+    o.kblk_stride = kTileElems * cs;
+  }
+  return o;
+}
+
 dev::OperandDesc rowmajor_operand(const void* base, long long ld_bytes, long long kbytes) {
   dev::OperandDesc o;
   o.base = static_cast<const char*>(base);
@@ -1317,13 +1337,8 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     p.q8_ldz = g.ld_k;
     p.cpos = cpos;
   }
-  // A = C, tile-blocked: rows of a 256x256 tile are 256 elements; every 256 K-columns jump
-  // to the next tile of the row panel.
-  p.A.base = static_cast<const char*>(sc);
-  p.A.ld = kTile * cs;
-  p.A.row_tile_stride = (long long)g.col_tiles * kTileElems * cs;
-  p.A.kblk = kTile * cs;
-  p.A.kblk_stride = kTileElems * cs;
+  // A = C, tile-blocked (coef_tile_operand)
+  p.A = coef_tile_operand(sc, g.col_tiles, cs);
   // B = ZqT_all [W][dim_n][ld_t]: rows = embedding dims, K = global columns, one K block per rank.
   p.B.base = static_cast<const char*>(zqt_all);
   const long long ldt = f8 ? q8_ldt(g) : g.ld_t;
@@ -1380,11 +1395,7 @@ void launch_dz_view(DType comp, const void* a, long long a_panel_tiles, const vo
   NTXENT_CHECK(k_tiles > 0 && a_panel_tiles >= k_tiles, "dz_view: bad K extent");
   const long long cs = (long long)dtype_size(comp);
   dev::SimParams p = base_params(g);
-  p.A.base = static_cast<const char*>(a);
-  p.A.ld = kTile * cs;
-  p.A.row_tile_stride = a_panel_tiles * kTileElems * cs;
-  p.A.kblk = kTile * cs;
-  p.A.kblk_stride = kTileElems * cs;
+  p.A = coef_tile_operand(a, a_panel_tiles, cs);
   // B: K blocks of transposed rows (rows = embedding dims, ld_t apart), one block per rank
   NTXENT_CHECK(b_kblk_cols > 0 && b_kblk_cols % kTile == 0, "dz_view: bad B K block");
   p.B.base = static_cast<const char*>(b);

@@ -41,6 +41,24 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 6
 #define NTXENT_GEMM_DMA_AUX 0
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
+// Coefficient-tile layout (experiment switch, tools/build_variant.sh -DNTXENT_C_KB=1): 0 =
+// row-major 256 x 256 per tile; 1 = K-step blocked: the 128-byte K-step column blocks of a tile
+// are consecutive 32 KiB blocks [kstep][row][128 B], so one dZ K-step of a 256-row panel is one
+// contiguous 32 KiB read (and a 64-column coefficient region one contiguous 8 KiB store).
+#ifndef NTXENT_C_KB
+#define NTXENT_C_KB 0
+#endif
+// L2 prefetch distance of the dZ GEMM (experiment switch: 0 = off): every K-step each wave issues
+// one 4-byte LDS-DMA per 128-byte line of 64 operand rows of K-step ks + D into an LDS sink, so
+// the staging DMA of that K-step later hits the XCD's L2.
+#ifndef NTXENT_DZ_PREFETCH
+#define NTXENT_DZ_PREFETCH 0
+#endif
+// Byte offset of element (r, c) inside a coefficient tile of es-byte elements (NTXENT_C_KB).
+__device__ __forceinline__ long long ctile_off(int r, int c, int es) {
+  if (NTXENT_C_KB) return (long long)((c * es) >> 7) * (kTile * kKStepBytes) + r * kKStepBytes + ((c * es) & 127);
+  return ((long long)r * kTile + c) * es;
+}
 constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
@@ -236,9 +254,11 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
                                                                      (row_t0 - row_base) * 2) = pk.u;
       } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) slot[(row_t0 + r) * kTile + col_t] = c[ni][r];
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<float*>(reinterpret_cast<char*>(slot) + ctile_off(row_t0 + r, col_t, 4)) = c[ni][r];
         if (mirror)
-          *reinterpret_cast<f32x4*>(mirror + col_t * kTile + row_t0) = f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
+          *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(mirror) + ctile_off(col_t, row_t0, 4)) =
+              f32x4{c[ni][0], c[ni][1], c[ni][2], c[ni][3]};
       }
     }
   }
@@ -267,8 +287,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         const int k = tid + NT * q;
         const int row = k / CPR, c16 = k % CPR;
         const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(mirror) + (col_base + row) * (kTile * 2) + row_base * 2 +
-                                  c16 * 16) = v;
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(mirror) + ctile_off(col_base + row, row_base + 8 * c16, 2)) = v;
       }
     }
     // (b) rows of C = columns of Ct via the gfx950 transposed LDS read (ds_read_b64_tr_b16):
@@ -298,8 +317,8 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       u32x4 v;
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)u[k]);
-      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) + (row_base + c0 + (lane >> 2)) * (kTile * 2) +
-                                (col_base + (blk / RB) * 32 + 8 * (lane & 3)) * 2) = v;
+      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) +
+                                ctile_off(row_base + c0 + (lane >> 2), col_base + (blk / RB) * 32 + 8 * (lane & 3), 2)) = v;
     }
   }
 }
@@ -434,10 +453,10 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   for (int q = 0; q < 4; ++q) {
     const int row = (lane >> 2) + 16 * q, c16 = lane & 3;
     const u32x4 v = *(__attribute__((address_space(3))) const u32x4*)(ld_d + row * S8 + c16 * 16);
-    *reinterpret_cast<u32x4*>(slot + (row_base + row) * kTile + col_base + c16 * 16) = v;
+    *reinterpret_cast<u32x4*>(slot + ctile_off(row_base + row, col_base + c16 * 16, 1)) = v;
     if (mirror) {
       const u32x4 m = *(__attribute__((address_space(3))) const u32x4*)(ld_m + row * S8 + c16 * 16);
-      *reinterpret_cast<u32x4*>(mirror + (col_base + row) * kTile + row_base + c16 * 16) = m;
+      *reinterpret_cast<u32x4*>(mirror + ctile_off(col_base + row, row_base + c16 * 16, 1)) = m;
     }
   }
 }
@@ -787,6 +806,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   f32x4 acc[8][4];
   constexpr bool kF8 = std::is_same<T, fp8e4m3>::value;
+  constexpr int kPfDist = MODE == kModeDz && !kF8 ? NTXENT_DZ_PREFETCH : 0;  // L2 prefetch (l2_prefetch)
   // fp8: the MFMA runs with unit E8M0 scales (127); the rows' power-of-two scales are applied to
   // the accumulators before the epilogue (exact). Per-lane scale operands loaded per tile cost a
   // vmcnt(0) drain of the prologue DMA (a plain load's first use with LDS-DMA in flight).
@@ -897,7 +917,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   constexpr bool kStreamMode = MODE == kModeFwd && !kF8;
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
-  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
+  auto dma_wait = [&]() {
+    if constexpr (kPfDist > 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // + the prefetch
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  };
   // Wave group (0: waves 0-3, 1: waves 4-7); each SIMD hosts one wave of each group.
   const int grp = __builtin_amdgcn_readfirstlane(w) >> 2;
 
@@ -953,6 +976,22 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     tile = p.dp_tiles + stile;
     return true;
   };
+  // L2 prefetch (dZ, NTXENT_DZ_PREFETCH = D > 0): wave w touches rows 64 (w & 3) + lane of operand
+  // w >> 2 at K-step min(kb + s, ke - 1), one 4-byte LDS-DMA per 128-byte line into its own 256 B
+  // of the sink above the stage buffers (garbage nobody reads; the fused epilogue's row
+  // coefficients reuse that area only after the main loop's vmcnt(0)).
+  const char* pf_base = nullptr;  // this wave's operand panel of the current item
+  int pf_k0 = 0, pf_klast = 0;
+  auto l2_prefetch = [&](int s) {
+    if constexpr (kPfDist > 0) {
+      const OperandDesc& o = (w >> 2) ? p.B : p.A;
+      const int k = pf_k0 + s < pf_klast ? pf_k0 + s : pf_klast;
+      const long long kbyte = (long long)k * kKStepBytes;
+      const char* src = pf_base + (kbyte / o.kblk) * o.kblk_stride + kbyte % o.kblk +
+                        (long long)(64 * (w & 3) + lane) * o.ld;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kGemmLds + 256 * w), 4, 0, 0);
+    }
+  };
   // operand streams of an item + its prologue DMA: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1
   // (the stream clamps keep the trailing prefetches in bounds, so every wait count is uniform)
   auto prologue = [&](int tile, int kb, int ke) {
@@ -963,6 +1002,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(Ab, k0, p.A, ns); sa1.init(Ab, k0, p.A, ns);
     sb0.init(Bb, k0, p.B, ns); sb1.init(Bb, k0, p.B, ns);
+    if constexpr (kPfDist > 0) {
+      pf_base = (w >> 2) ? Bb : Ab;
+      pf_k0 = kb + kPfDist;
+      pf_klast = ke - 1;
+    }
     if constexpr (kF8 && MODE != kModeDz) {
       // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
       // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a
@@ -973,6 +1017,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
     stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
     stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
+    l2_prefetch(0);  // (in the steady state every phase-4 B1 stage is followed by one)
   };
   // Forward streaming needs whole-tile items with an even number of >= 2 K-steps (the streams
   // run two K-steps into the next item; even: its K-step 0 lands in buffer 0, as after a
@@ -1003,7 +1048,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
+  if constexpr (kPfDist > 0) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");  // A0(0), B0(0) retired
+  else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   barrier();
   if (grp == 1) barrier();  // stagger group 1 by one barrier
   for (int ks = 0; ks < nsteps; ++ks) {
@@ -1035,6 +1081,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     mma_quadrant(kI1, kI0, af, bf0);
     dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
+    l2_prefetch(ks + 1);            //   (dZ experiment switch; no instruction otherwise)
     barrier();                      // phase 4 C
     mma_quadrant(kI1, kI1, af, bf1);
   }
