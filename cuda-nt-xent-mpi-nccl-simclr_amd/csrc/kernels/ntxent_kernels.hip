@@ -1110,6 +1110,13 @@ int q8_ldt(const Geometry& g) { return g.rows_pad; }
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
 // partial slabs serially (BASELINE config 4: 36 tiles x 128 K-steps, fixup ~40 % of the GEMM).
+// K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel; experiment switch
+// NTXENT_DIAG_KS, 2 or 4)
+#ifndef NTXENT_DIAG_KS
+#define NTXENT_DIAG_KS 2
+#endif
+constexpr int kDiagKS = NTXENT_DIAG_KS;
+
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
   if (diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
   const int pcs = std::min(cus / ntiles, nk / 8);
@@ -1145,10 +1152,10 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   int nstrip = 0;
   if (diag_tail > 0 && !f8 && nk_tile >= 4) {
     const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
-    // 10 arrival tickets per tile in the counter region, 12 half-region fp32 partials per tile
-    // in the slab region
-    if (q >= 1 && rem > 0 && rem <= diag_tail && 10 * rem <= 2 * ws.num_cus &&
-        (size_t)12 * rem * 4096 <= (size_t)2 * ws.num_cus * kTileElems)
+    // 14 arrival tickets per tile in the counter region, 10 KS piece partials per tile in the
+    // slab region (diag_up_kernel)
+    if (q >= 1 && rem > 0 && rem <= diag_tail && 14 * rem <= 2 * ws.num_cus &&
+        (size_t)10 * kDiagKS * rem * 4096 <= (size_t)2 * ws.num_cus * kTileElems)
       nstrip = rem;
   }
   const int nmain = ntiles - nstrip;
@@ -1197,9 +1204,9 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // row-group partials in the column-partial area of the workspace
         float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                     (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
-        const dim3 sg(nstrip * 16);
-        if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1>), sg, dim3(256), 0, stream, q, scratch);
-        else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0>), sg, dim3(256), 0, stream, q, scratch);
+        const dim3 sg(nstrip * dev::diag_up_blocks<kDiagKS>());
+        if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, kDiagKS>), sg, dim3(256), 0, stream, q, scratch);
+        else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, kDiagKS>), sg, dim3(256), 0, stream, q, scratch);
       }
     }
   });
@@ -1321,6 +1328,23 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
   return true;
 }
 
+// Panel dot exchange of the fused dZ epilogue (dev::panel_dot_exchange): only where every tile of
+// a row panel is resident at once, i.e. the dZ launch is exactly one round of whole tiles (one
+// 512-thread block per CU, tiles == CUs, no split-K). Experiment switch NTXENT_DOT_EXCHANGE.
+#ifndef NTXENT_DOT_EXCHANGE
+#define NTXENT_DOT_EXCHANGE 0
+#endif
+bool dz_dot_exchange(const Geometry& g, DType comp, const GemmWorkspace& ws) {
+  if (!NTXENT_DOT_EXCHANGE || comp == DType::F32 || comp == DType::FP8 || g.dim % 8 != 0) return false;
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+  const int ntiles = g.row_tiles * (g.dim_n / kTile);
+  const int nk = (int)((long long)g.world * g.rows_pad * dtype_size(comp) / kKStepBytes);
+  if (ntiles != cus || fwd_splitk_pieces(ntiles, nk, cus, 1) >= 3) return false;
+  // counters [2][row_tiles] in the counter region, partials [Rpad][dim_n / 256] in the slab region
+  return 2 * g.row_tiles <= 2 * ws.num_cus &&
+         (size_t)g.rows_pad * (g.dim_n / kTile) <= (size_t)2 * ws.num_cus * kTileElems;
+}
+
 bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
                void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
                const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
@@ -1378,6 +1402,13 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     grid = apply_schedule(p, ntiles, ws, stream);
   }
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
+  if (fused && pieces == 0 && ntiles == g.row_tiles * (g.dim_n / kTile) && dz_dot_exchange(g, comp, ws)) {
+    NTXENT_CHECK(grid == ntiles && p.sk_tiles == 0 && ws.ptr != nullptr, "dz: dot exchange needs a one-round launch");
+    p.dot_cnt = static_cast<int*>(ws.ptr);
+    p.dot_x = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
+  } else if (fused) {
+    NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot (and no dot exchange)");
+  }
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);

@@ -51,6 +51,11 @@ constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
 // L2 prefetch distance of the dZ GEMM (experiment switch: 0 = off): every K-step each wave issues
 // one 4-byte LDS-DMA per 128-byte line of 64 operand rows of K-step ks + D into an LDS sink, so
 // the staging DMA of that K-step later hits the XCD's L2.
+// Kept-cosine stores of the forward GEMM epilogue (experiment switch): 0 = default policy, 1 =
+// non-temporal (the tiles are re-read only by the coefficient pass, after the whole forward)
+#ifndef NTXENT_COS_NT
+#define NTXENT_COS_NT 0
+#endif
 #ifndef NTXENT_DZ_PREFETCH
 #define NTXENT_DZ_PREFETCH 0
 #endif
@@ -101,7 +106,10 @@ struct SimParams {
   const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
   int nh_dt, nd;
   const float* ninv;     // ... 1 / |h_i|
-  const float* ndot;     // ... dot_i (reduced dotp)
+  const float* ndot;     // ... dot_i (reduced dotp); unused with dot_x:
+  float* dot_x;          // ... panel exchange (dz_store): [row_tiles][dim_n / 256][256] partials of
+                         //     z.g over each tile's columns, summed by every tile of the row panel
+  int* dot_cnt;          // ... [2][row_tiles] arrival / departure counters (zero; self-cleaning)
   const float* ngo;      // ... grad_out (device scalar)
   float nalpha;          // ... 1 / (2N tau)
   void* ndh;             // ... output dh [R][nd] (non-null: fused epilogue)
@@ -623,6 +631,96 @@ __device__ __forceinline__ void dz8_finish(f32x4 (&acc)[8][4], const SimParams& 
   }
 }
 
+// dot_m = z_m . g_m for the fused normalisation backward, from the dZ tiles themselves: every tile
+// (mt, nt) of row panel mt sums h_m . g_m over its 256 columns (g: the fp16 tile staged in `lds`,
+// h: this thread's chunks hq, or fp32 rows from memory), publishes the 256 row partials, and waits
+// until all dim_n / 256 tiles of the panel have; then each sums the panel's partials in column-tile
+// order (deterministic) and returns, for thread tid < 256, sum_n h_(m0 + tid) . g = dot / inv.
+// Hand-off (MI355X_MICROARCH.md, Valid forms row 1): write-through (sc1) 4-byte partial stores,
+// every storing wave drained (vmcnt(0)), a workgroup barrier, one agent-scope counter add per
+// tile; the consumer polls the counter with sc1 loads and reads every partial with sc1 loads.
+// Requires every tile of a panel to be resident at once: launch_dz enables it only for one-round
+// launches (one tile per block, grid <= CUs, one 512-thread block per CU). A departure counter
+// returns both counters to zero once all tiles of the panel have read, so the workspace serves the
+// next launch. The spin is bounded: on timeout the partial is NaN, which poisons dh visibly.
+__device__ __forceinline__ float panel_dot_exchange(const SimParams& p, int mt, int nt, int tid, lds_char* lds,
+                                                   const u32x4 (&hq)[16]) {
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  const int NT = p.ldo / kTile;  // column tiles of a row panel (dim_n / 256)
+  const int lane = tid & 63;
+  float pd[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
+    const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
+    float acc = 0.f;
+    if (m < p.R && d0 < p.nd) {
+      union { _Float16 h[8]; u32x4 u; } g;
+      g.u = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
+      float hv[8];
+      if (p.nh_dt == 2) {
+        union { __bf16 h[8]; u32x4 u; } x;
+        x.u = hq[k];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
+      } else if (p.nh_dt == 1) {
+        union { _Float16 h[8]; u32x4 u; } x;
+        x.u = hq[k];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
+      } else {
+        const f32x4* hp = reinterpret_cast<const f32x4*>(static_cast<const float*>(p.nh) + (long long)m * p.nd + d0);
+        const f32x4 a0 = hp[0], a1 = hp[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { hv[e] = a0[e]; hv[4 + e] = a1[e]; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += (float)g.h[e] * hv[e];
+    }
+    // the 32 threads of a row (a half wave: c = lane & 31) in a fixed tree
+    acc = row16_sum(acc);
+    acc += __shfl_xor(acc, 16, 64);
+    pd[k] = acc;
+  }
+  int* cnt = p.dot_cnt + mt;                   // arrivals of the panel's tiles
+  int* dep = p.dot_cnt + (p.Rpad / kTile) + mt;  // departures
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc(p.dot_x + (size_t)mt * NT * kTile, 0, NT * kTile * 4, 0x00020000);
+  if ((lane & 31) == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pd[k]), xrs, (nt * kTile + (tid >> 5) + 16 * k) * 4, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  typedef __attribute__((address_space(3))) int lds_int;
+  lds_int* flag = (lds_int*)(lds + kTile * 512 + 2048 - 16);  // in the cf area, written only after this
+  if (tid == 0) {
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 0;
+    for (int it = 0; it < (1 << 22); ++it) {
+      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= NT) { ok = 1; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *flag = ok;
+  }
+  __syncthreads();
+  const bool ok = *flag != 0;
+  float dot = 0.f;
+  if (tid < kTile) {
+    for (int j = 0; j < NT; ++j)
+      dot += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (j * kTile + tid) * 4, 0, 16));
+  }
+  __syncthreads();  // every partial read: the counters may return to zero
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(dep, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == NT - 1) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(dep, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return ok ? dot : __builtin_nanf("");
+}
+
 // dZ epilogue (swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r])
 // of output tile (mt, nt); `lds` (>= 128 KiB, free) stages the fp16 tile for coalesced rows.
 __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
@@ -642,7 +740,7 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
     float iv0 = 0.f, dt0 = 0.f;
     if (p.ndh && tid < kTile && mt * kTile + tid < p.R) {
       iv0 = p.ninv[mt * kTile + tid];
-      dt0 = p.ndot[mt * kTile + tid];
+      if (!p.dot_x) dt0 = p.ndot[mt * kTile + tid];
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -677,6 +775,7 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
       const float sgo = p.ngo[0] * p.nalpha;
       typedef __attribute__((address_space(3))) float lds_fl;
       lds_fl* cf = (lds_fl*)(lds + kTile * 512);  // [256][2] per-row c1, c2
+      if (p.dot_x) dt0 = iv0 * panel_dot_exchange(p, mt, nt, tid, lds, hq);
       if (tid < kTile) {
         cf[2 * tid] = sgo * iv0;
         cf[2 * tid + 1] = sgo * iv0 * iv0 * dt0;
@@ -1159,7 +1258,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
             pk.h[r] = from_f32<TS>(acc[mi][2 * np][r]);
             pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r]);
           }
-          *reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8) = pk.u;
+          u32x4* dst = reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8);
+          if constexpr (NTXENT_COS_NT) __builtin_nontemporal_store(pk.u, dst);
+          else *dst = pk.u;
         } else {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
@@ -1415,8 +1516,12 @@ constexpr int kSubStages = 3;
 // loop is bound by load latency over the few K-steps in flight, so the diagonal-region blocks
 // (half the rows per K-step) run a 6-stage ring of 8 KiB stages in the same LDS (5 in flight).
 // ------------------------------------------------------------------------------------
+// KS: K pieces of an off-diagonal region (a diagonal region gets KS / 2, at least 1); the pieces'
+// fp32 partials go to write-through slabs and the last piece to arrive (ticket) sums them in piece
+// order. 4 + 10 tickets and 10 KS 16 KiB slabs per tile (launch_fwd_stats checks the workspace).
 constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + column-partial exchange + flags
-template <typename T, int FX>
+template <int KS> constexpr int diag_up_blocks() { return 4 * (KS / 2 > 1 ? KS / 2 : 1) + 6 * KS; }
+template <typename T, int FX, int KS>
 __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch) {
   using MM = Mfma<T>;
   typedef typename MM::frag frag;
@@ -1425,17 +1530,22 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   lds_char* lds = (lds_char*)smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nt_d = gridDim.x >> 4;                    // diagonal tiles in this launch
-  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's 16 blocks share one XCD
-  const int tile = idx >> 4, s = idx & 15;
-  const bool dg = s < 4;
-  const int q = dg ? 0 : (s - 4) >> 1, hk = dg ? 0 : (s - 4) & 1;
-  const int a = dg ? s : (q < 3 ? 0 : (q < 5 ? 1 : 2));
-  const int b = dg ? s : (q < 3 ? q + 1 : (q < 5 ? q - 1 : 3));
+  constexpr int KSD = KS / 2 > 1 ? KS / 2 : 1;        // K pieces of a diagonal region
+  constexpr int NB = diag_up_blocks<KS>();            // blocks per tile
+  const int nt_d = gridDim.x / NB;                    // diagonal tiles in this launch
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's blocks share one XCD
+  const int tile = idx / NB, s = idx % NB;
+  const bool dg = s < 4 * KSD;
+  const int q = dg ? 0 : (s - 4 * KSD) / KS;                     // off-diagonal pair 0..5
+  const int hk = dg ? s % KSD : (s - 4 * KSD) % KS;               // K piece
+  const int nkp = dg ? KSD : KS;                                  // pieces of this region
+  const int rq = dg ? s / KSD : 4 + q;                            // region slot 0..9
+  const int a = dg ? s / KSD : (q < 3 ? 0 : (q < 5 ? 1 : 2));
+  const int b = dg ? s / KSD : (q < 3 ? q + 1 : (q < 5 ? q - 1 : 3));
   const int4 t = p.tiles[tile];
   const int mt = t.x, nt = t.y;
   const int nk = (int)(p.kbytes / kKStepBytes);
-  const int k0 = dg ? 0 : (hk == 0 ? 0 : nk / 2), k1 = dg ? nk : (hk == 0 ? nk / 2 : nk);
+  const int k0 = nk * hk / nkp, k1 = nk * (hk + 1) / nkp;
   // DMA pieces: diagonal region 2 per wave (ring rows 16 w + 8 j + (lane >> 3) = A rows 64 a..),
   // off-diagonal 4 per wave (ring rows 32 w + 8 j + ..: 0-63 A = rows 64 a.., 64-127 B = 64 b..)
   const int np = dg ? 2 : 4;
@@ -1496,11 +1606,13 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
   int* flag = reinterpret_cast<int*>(smem + kSubStages * kSubStage + 4 * 64 * 8);
-  int* cnt_pair = p.sk_cnt + 4 * nt_d;  // [nt_d][6] after the [nt_d][4] row-group tickets
-  if (!dg) {
-    // K halves: publish this half's fp32 partial (write-through), the second to arrive adds it
-    const auto prs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs + (size_t)((tile * 6 + q) * 2) * 4096, 0,
-                                                      2 * 4096 * 4, 0x00020000);
+  int* cnt_pair = p.sk_cnt + 4 * nt_d;  // [nt_d][10] after the [nt_d][4] row-group tickets
+  if (nkp > 1) {
+    // K pieces: publish this piece's fp32 partial (write-through); the last to arrive sums the
+    // region's pieces in piece order (its own from registers), so the result does not depend on
+    // the arrival order
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(p.sk_slabs + (size_t)((tile * 10 + rq) * KS) * 4096, 0,
+                                                      KS * 4096 * 4, 0x00020000);
 #pragma unroll
     for (int f = 0; f < 4; ++f)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[f]), prs,
@@ -1508,19 +1620,27 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(cnt_pair + tile * 6 + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == 1;
-      if (last) __hip_atomic_store(cnt_pair + tile * 6 + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int old = __hip_atomic_fetch_add(cnt_pair + tile * 10 + rq, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == nkp - 1;
+      if (last) __hip_atomic_store(cnt_pair + tile * 10 + rq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = last;
     }
     __syncthreads();
     if (!flag[0]) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    f32x4 sum[4];
+    for (int h = 0; h < nkp; ++h) {
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(((1 - hk) * 4096 + ((w * 4 + f) * 64 + lane) * 4) * 4), 0, 16);
-      acc[f] += __builtin_bit_cast(f32x4, v);  // fp32 addition commutes: either arrival order, same bits
+      for (int f = 0; f < 4; ++f) {
+        f32x4 v = acc[f];
+        if (h != hk)
+          v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            prs, (int)((h * 4096 + ((w * 4 + f) * 64 + lane) * 4) * 4), 0, 16));
+        sum[f] = h == 0 ? v : sum[f] + v;
+      }
     }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) acc[f] = sum[f];
   }
   // lane holds S[row 64a + 16w + 4 (lane >> 4) + r][col 64b + 16 f + (lane & 15)] (tile-local)
   const int rb0 = 64 * a + 16 * w;
