@@ -286,11 +286,6 @@ struct NormFuse {
   const float* grad_out = nullptr;  // device scalar
   void* dh = nullptr;
 };
-// dz_dot_exchange: whether launch_dz(comp, ..., nf) on the plan's dZ tiles computes dot_i itself
-// (the tiles of a row panel exchange their partials of z_i . g_i; one-round launches only): the
-// coefficient pass then needs no dot partials, launch_dot_reduce is skipped and NormFuse::dot may
-// be null. It also lets fp8-forward plans fuse (their kept cosines are e4m3-rounded).
-bool dz_dot_exchange(const Geometry& g, DType comp, const GemmWorkspace& ws);
 // comp = FP8 with q8: the fp8 backward's dZ (cbuf = e4m3 C tiles, zqt_all = Q8Stats::zq8t;
 // block-scaled MFMA, per-row dequantisation and the exact positive term in the epilogue).
 bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,

@@ -790,21 +790,14 @@ int padded_ld(int n) { return (n % 1024 == 0) ? n + 64 : n; }
 
 // The coefficient tiles as the dZ GEMM's A operand: tile (I, J) of a row panel of `panel_tiles`
 // tiles; 256 K-columns per tile. Row-major tiles: rows of 256 elements, every 256 K-columns jump
-// to the next tile of the panel. K-step-blocked tiles (NTXENT_C_KB, dev::ctile_off): a K-step of
-// a row panel is one 32 KiB block [256 rows][128 B] and the K-steps of a panel follow each other.
+// to the next tile of the panel.
 dev::OperandDesc coef_tile_operand(const void* base, long long panel_tiles, long long cs) {
   dev::OperandDesc o;
   o.base = static_cast<const char*>(base);
   o.row_tile_stride = panel_tiles * kTileElems * cs;
-  if (NTXENT_C_KB) {
-    o.ld = kKStepBytes;
-    o.kblk = kKStepBytes;
-    o.kblk_stride = (long long)kTile * kKStepBytes;
-  } else {
-    o.ld = kTile * cs;
-    o.kblk = kTile * cs;
-    o.kblk_stride = kTileElems * cs;
-  }
+  o.ld = kTile * cs;
+  o.kblk = kTile * cs;
+  o.kblk_stride = kTileElems * cs;
   return o;
 }
 
@@ -1107,15 +1100,13 @@ bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
 int q8_ldt(const Geometry& g) { return g.rows_pad; }
 
+// K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel; 4 pieces measured
+// +6 us at config 5, neutral at the headline: profiles/r4/variants_r4_v2.md)
+constexpr int kDiagKS = 2;
+
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
 // partial slabs serially (BASELINE config 4: 36 tiles x 128 K-steps, fixup ~40 % of the GEMM).
-// K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel; experiment switch
-// NTXENT_DIAG_KS, 2 or 4)
-#ifndef NTXENT_DIAG_KS
-#define NTXENT_DIAG_KS 2
-#endif
-constexpr int kDiagKS = NTXENT_DIAG_KS;
 
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
   if (diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
@@ -1140,6 +1131,9 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.kbytes = kb;
   p.part = part;
   p.sc = static_cast<char*>(sc);
+  // kept tiles beyond half the 256 MiB MALL: non-temporal stores (config 5, 260 MiB: coefficient
+  // pass -10 us, dZ -4 us; at 66 MiB the default policy is 4 us faster: profiles/r4/variants_r4_v2.md)
+  p.sc_nt = (long long)ntiles * kTileElems * (comp == DType::F32 ? 4 : 2) > (128ll << 20) ? 1 : 0;
   p.b_tile0 = bv.b_tile0;
   p.part_x = part_x;
   const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
@@ -1328,23 +1322,6 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
   return true;
 }
 
-// Panel dot exchange of the fused dZ epilogue (dev::panel_dot_exchange): only where every tile of
-// a row panel is resident at once, i.e. the dZ launch is exactly one round of whole tiles (one
-// 512-thread block per CU, tiles == CUs, no split-K). Experiment switch NTXENT_DOT_EXCHANGE.
-#ifndef NTXENT_DOT_EXCHANGE
-#define NTXENT_DOT_EXCHANGE 0
-#endif
-bool dz_dot_exchange(const Geometry& g, DType comp, const GemmWorkspace& ws) {
-  if (!NTXENT_DOT_EXCHANGE || comp == DType::F32 || comp == DType::FP8 || g.dim % 8 != 0) return false;
-  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
-  const int ntiles = g.row_tiles * (g.dim_n / kTile);
-  const int nk = (int)((long long)g.world * g.rows_pad * dtype_size(comp) / kKStepBytes);
-  if (ntiles != cus || fwd_splitk_pieces(ntiles, nk, cus, 1) >= 3) return false;
-  // counters [2][row_tiles] in the counter region, partials [Rpad][dim_n / 256] in the slab region
-  return 2 * g.row_tiles <= 2 * ws.num_cus &&
-         (size_t)g.rows_pad * (g.dim_n / kTile) <= (size_t)2 * ws.num_cus * kTileElems;
-}
-
 bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
                void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
                const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
@@ -1402,13 +1379,7 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     grid = apply_schedule(p, ntiles, ws, stream);
   }
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
-  if (fused && pieces == 0 && ntiles == g.row_tiles * (g.dim_n / kTile) && dz_dot_exchange(g, comp, ws)) {
-    NTXENT_CHECK(grid == ntiles && p.sk_tiles == 0 && ws.ptr != nullptr, "dz: dot exchange needs a one-round launch");
-    p.dot_cnt = static_cast<int*>(ws.ptr);
-    p.dot_x = reinterpret_cast<float*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus));
-  } else if (fused) {
-    NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot (and no dot exchange)");
-  }
+  if (fused) NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot");
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);

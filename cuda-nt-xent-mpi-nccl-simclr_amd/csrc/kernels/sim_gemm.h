@@ -41,29 +41,9 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 6
 #define NTXENT_GEMM_DMA_AUX 0
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
-// Coefficient-tile layout (experiment switch, tools/build_variant.sh -DNTXENT_C_KB=1): 0 =
-// row-major 256 x 256 per tile; 1 = K-step blocked: the 128-byte K-step column blocks of a tile
-// are consecutive 32 KiB blocks [kstep][row][128 B], so one dZ K-step of a 256-row panel is one
-// contiguous 32 KiB read (and a 64-column coefficient region one contiguous 8 KiB store).
-#ifndef NTXENT_C_KB
-#define NTXENT_C_KB 0
-#endif
-// L2 prefetch distance of the dZ GEMM (experiment switch: 0 = off): every K-step each wave issues
-// one 4-byte LDS-DMA per 128-byte line of 64 operand rows of K-step ks + D into an LDS sink, so
-// the staging DMA of that K-step later hits the XCD's L2.
-// Kept-cosine stores of the forward GEMM epilogue (experiment switch): 0 = default policy, 1 =
-// non-temporal (the tiles are re-read only by the coefficient pass, after the whole forward)
-#ifndef NTXENT_COS_NT
-#define NTXENT_COS_NT 0
-#endif
-#ifndef NTXENT_DZ_PREFETCH
-#define NTXENT_DZ_PREFETCH 0
-#endif
-// Byte offset of element (r, c) inside a coefficient tile of es-byte elements (NTXENT_C_KB).
-__device__ __forceinline__ long long ctile_off(int r, int c, int es) {
-  if (NTXENT_C_KB) return (long long)((c * es) >> 7) * (kTile * kKStepBytes) + r * kKStepBytes + ((c * es) & 127);
-  return ((long long)r * kTile + c) * es;
-}
+// Byte offset of element (r, c) inside a row-major 256 x 256 coefficient tile of es-byte
+// elements. (A K-step-blocked layout, [kstep][row][128 B], measured neutral: profiles/r4/variants.)
+__device__ __forceinline__ long long ctile_off(int r, int c, int es) { return ((long long)r * kTile + c) * es; }
 constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
@@ -91,6 +71,8 @@ struct SimParams {
   int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
   char* sc;              // kept cosines: [n_fwd_tiles][256*256] (canonical fragment order)
+  int sc_nt;             // 1: kept-cosine stores are non-temporal (set when the kept tiles exceed
+                         //    half the MALL: they are re-read only by the coefficient pass)
   char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
   const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
   const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
@@ -106,10 +88,7 @@ struct SimParams {
   const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
   int nh_dt, nd;
   const float* ninv;     // ... 1 / |h_i|
-  const float* ndot;     // ... dot_i (reduced dotp); unused with dot_x:
-  float* dot_x;          // ... panel exchange (dz_store): [row_tiles][dim_n / 256][256] partials of
-                         //     z.g over each tile's columns, summed by every tile of the row panel
-  int* dot_cnt;          // ... [2][row_tiles] arrival / departure counters (zero; self-cleaning)
+  const float* ndot;     // ... dot_i (reduced dotp)
   const float* ngo;      // ... grad_out (device scalar)
   float nalpha;          // ... 1 / (2N tau)
   void* ndh;             // ... output dh [R][nd] (non-null: fused epilogue)
@@ -631,96 +610,6 @@ __device__ __forceinline__ void dz8_finish(f32x4 (&acc)[8][4], const SimParams& 
   }
 }
 
-// dot_m = z_m . g_m for the fused normalisation backward, from the dZ tiles themselves: every tile
-// (mt, nt) of row panel mt sums h_m . g_m over its 256 columns (g: the fp16 tile staged in `lds`,
-// h: this thread's chunks hq, or fp32 rows from memory), publishes the 256 row partials, and waits
-// until all dim_n / 256 tiles of the panel have; then each sums the panel's partials in column-tile
-// order (deterministic) and returns, for thread tid < 256, sum_n h_(m0 + tid) . g = dot / inv.
-// Hand-off (MI355X_MICROARCH.md, Valid forms row 1): write-through (sc1) 4-byte partial stores,
-// every storing wave drained (vmcnt(0)), a workgroup barrier, one agent-scope counter add per
-// tile; the consumer polls the counter with sc1 loads and reads every partial with sc1 loads.
-// Requires every tile of a panel to be resident at once: launch_dz enables it only for one-round
-// launches (one tile per block, grid <= CUs, one 512-thread block per CU). A departure counter
-// returns both counters to zero once all tiles of the panel have read, so the workspace serves the
-// next launch. The spin is bounded: on timeout the partial is NaN, which poisons dh visibly.
-__device__ __forceinline__ float panel_dot_exchange(const SimParams& p, int mt, int nt, int tid, lds_char* lds,
-                                                   const u32x4 (&hq)[16]) {
-  typedef __attribute__((address_space(3))) u32x4 lds_u4;
-  const int NT = p.ldo / kTile;  // column tiles of a row panel (dim_n / 256)
-  const int lane = tid & 63;
-  float pd[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
-    const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
-    float acc = 0.f;
-    if (m < p.R && d0 < p.nd) {
-      union { _Float16 h[8]; u32x4 u; } g;
-      g.u = *(lds_u4*)(lds + rt * 512 + ((c ^ (rt & 15)) << 4));
-      float hv[8];
-      if (p.nh_dt == 2) {
-        union { __bf16 h[8]; u32x4 u; } x;
-        x.u = hq[k];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
-      } else if (p.nh_dt == 1) {
-        union { _Float16 h[8]; u32x4 u; } x;
-        x.u = hq[k];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = (float)x.h[e];
-      } else {
-        const f32x4* hp = reinterpret_cast<const f32x4*>(static_cast<const float*>(p.nh) + (long long)m * p.nd + d0);
-        const f32x4 a0 = hp[0], a1 = hp[1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { hv[e] = a0[e]; hv[4 + e] = a1[e]; }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc += (float)g.h[e] * hv[e];
-    }
-    // the 32 threads of a row (a half wave: c = lane & 31) in a fixed tree
-    acc = row16_sum(acc);
-    acc += __shfl_xor(acc, 16, 64);
-    pd[k] = acc;
-  }
-  int* cnt = p.dot_cnt + mt;                   // arrivals of the panel's tiles
-  int* dep = p.dot_cnt + (p.Rpad / kTile) + mt;  // departures
-  const auto xrs = __builtin_amdgcn_make_buffer_rsrc(p.dot_x + (size_t)mt * NT * kTile, 0, NT * kTile * 4, 0x00020000);
-  if ((lane & 31) == 0) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pd[k]), xrs, (nt * kTile + (tid >> 5) + 16 * k) * 4, 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  typedef __attribute__((address_space(3))) int lds_int;
-  lds_int* flag = (lds_int*)(lds + kTile * 512 + 2048 - 16);  // in the cf area, written only after this
-  if (tid == 0) {
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 0;
-    for (int it = 0; it < (1 << 22); ++it) {
-      if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= NT) { ok = 1; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    *flag = ok;
-  }
-  __syncthreads();
-  const bool ok = *flag != 0;
-  float dot = 0.f;
-  if (tid < kTile) {
-    for (int j = 0; j < NT; ++j)
-      dot += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, (j * kTile + tid) * 4, 0, 16));
-  }
-  __syncthreads();  // every partial read: the counters may return to zero
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(dep, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == NT - 1) {
-      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(dep, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  return ok ? dot : __builtin_nanf("");
-}
-
 // dZ epilogue (swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r])
 // of output tile (mt, nt); `lds` (>= 128 KiB, free) stages the fp16 tile for coalesced rows.
 __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
@@ -740,7 +629,7 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
     float iv0 = 0.f, dt0 = 0.f;
     if (p.ndh && tid < kTile && mt * kTile + tid < p.R) {
       iv0 = p.ninv[mt * kTile + tid];
-      if (!p.dot_x) dt0 = p.ndot[mt * kTile + tid];
+      dt0 = p.ndot[mt * kTile + tid];
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -775,7 +664,6 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
       const float sgo = p.ngo[0] * p.nalpha;
       typedef __attribute__((address_space(3))) float lds_fl;
       lds_fl* cf = (lds_fl*)(lds + kTile * 512);  // [256][2] per-row c1, c2
-      if (p.dot_x) dt0 = iv0 * panel_dot_exchange(p, mt, nt, tid, lds, hq);
       if (tid < kTile) {
         cf[2 * tid] = sgo * iv0;
         cf[2 * tid + 1] = sgo * iv0 * iv0 * dt0;
@@ -905,7 +793,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   f32x4 acc[8][4];
   constexpr bool kF8 = std::is_same<T, fp8e4m3>::value;
-  constexpr int kPfDist = MODE == kModeDz && !kF8 ? NTXENT_DZ_PREFETCH : 0;  // L2 prefetch (l2_prefetch)
   // fp8: the MFMA runs with unit E8M0 scales (127); the rows' power-of-two scales are applied to
   // the accumulators before the epilogue (exact). Per-lane scale operands loaded per tile cost a
   // vmcnt(0) drain of the prologue DMA (a plain load's first use with LDS-DMA in flight).
@@ -1016,10 +903,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   constexpr bool kStreamMode = MODE == kModeFwd && !kF8;
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
-  auto dma_wait = [&]() {
-    if constexpr (kPfDist > 0) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // + the prefetch
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  };
+  auto dma_wait = [&]() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); };
   // Wave group (0: waves 0-3, 1: waves 4-7); each SIMD hosts one wave of each group.
   const int grp = __builtin_amdgcn_readfirstlane(w) >> 2;
 
@@ -1075,22 +959,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     tile = p.dp_tiles + stile;
     return true;
   };
-  // L2 prefetch (dZ, NTXENT_DZ_PREFETCH = D > 0): wave w touches rows 64 (w & 3) + lane of operand
-  // w >> 2 at K-step min(kb + s, ke - 1), one 4-byte LDS-DMA per 128-byte line into its own 256 B
-  // of the sink above the stage buffers (garbage nobody reads; the fused epilogue's row
-  // coefficients reuse that area only after the main loop's vmcnt(0)).
-  const char* pf_base = nullptr;  // this wave's operand panel of the current item
-  int pf_k0 = 0, pf_klast = 0;
-  auto l2_prefetch = [&](int s) {
-    if constexpr (kPfDist > 0) {
-      const OperandDesc& o = (w >> 2) ? p.B : p.A;
-      const int k = pf_k0 + s < pf_klast ? pf_k0 + s : pf_klast;
-      const long long kbyte = (long long)k * kKStepBytes;
-      const char* src = pf_base + (kbyte / o.kblk) * o.kblk_stride + kbyte % o.kblk +
-                        (long long)(64 * (w & 3) + lane) * o.ld;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kGemmLds + 256 * w), 4, 0, 0);
-    }
-  };
   // operand streams of an item + its prologue DMA: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1
   // (the stream clamps keep the trailing prefetches in bounds, so every wait count is uniform)
   auto prologue = [&](int tile, int kb, int ke) {
@@ -1101,11 +969,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(Ab, k0, p.A, ns); sa1.init(Ab, k0, p.A, ns);
     sb0.init(Bb, k0, p.B, ns); sb1.init(Bb, k0, p.B, ns);
-    if constexpr (kPfDist > 0) {
-      pf_base = (w >> 2) ? Bb : Ab;
-      pf_k0 = kb + kPfDist;
-      pf_klast = ke - 1;
-    }
     if constexpr (kF8 && MODE != kModeDz) {
       // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
       // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a
@@ -1116,7 +979,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
     stage(0, 0, sa0, 0); stage(1, 0, sb0, 0); stage(1, 1, sb1, 0); stage(0, 1, sa1, 0);
     stage(0, 0, sa0, 1); stage(1, 0, sb0, 1); stage(1, 1, sb1, 1);
-    l2_prefetch(0);  // (in the steady state every phase-4 B1 stage is followed by one)
   };
   // Forward streaming needs whole-tile items with an even number of >= 2 K-steps (the streams
   // run two K-steps into the next item; even: its K-step 0 lands in buffer 0, as after a
@@ -1147,8 +1009,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if constexpr (kPfDist > 0) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");  // A0(0), B0(0) retired
-  else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
   if (grp == 1) barrier();  // stagger group 1 by one barrier
   for (int ks = 0; ks < nsteps; ++ks) {
@@ -1180,7 +1041,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     mma_quadrant(kI1, kI0, af, bf0);
     dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
-    l2_prefetch(ks + 1);            //   (dZ experiment switch; no instruction otherwise)
     barrier();                      // phase 4 C
     mma_quadrant(kI1, kI1, af, bf1);
   }
@@ -1259,7 +1119,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
             pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r]);
           }
           u32x4* dst = reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8);
-          if constexpr (NTXENT_COS_NT) __builtin_nontemporal_store(pk.u, dst);
+          if (p.sc_nt) __builtin_nontemporal_store(pk.u, dst);
           else *dst = pk.u;
         } else {
 #pragma unroll

@@ -52,11 +52,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   // normalisation backward fused into the dZ epilogue (the coefficient pass emits dot partials;
   // the symmetric mode sums received contributions in launch_norm_bwd instead)
   // (not on fp8 plans: dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines, ~1e-2 off)
-  // (fp8-forward plans fuse only with the dZ epilogue's own dot exchange: dot_i = sum_j C_ij cos_ij
-  // from the coefficient pass would use the e4m3 forward's cosines)
-  ws_.num_cus = device_info(device_).num_cus;
-  xdot_ = !small_ && !symm_ && !q8_ && dz_dot_exchange(g_, bwd_, ws_);
-  fuse_ = !small_ && !symm_ && !q8_ && bwd_ != DType::F32 && g_.dim % 8 == 0 && (!f8_ || xdot_);
+  fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && g_.dim % 8 == 0;
 
   const auto ft = symm_ ? build_sym_fwd_tiles(g_, jobs_, nch_) : build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -92,8 +88,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&contrib_, symm_ ? (jobs_.size() + 1) * Rp * g_.dim_n * ccs_ : 0},
       {(void**)&recv_, symm_ && ccs_ == 2 ? inc_.size() * Rp * g_.dim_n * ccs_ : 0},
       {(void**)&dz_rows_, symm_ ? (size_t)4 * (world_ + 1) * g_.row_tiles * (g_.dim_n / kTile) * sizeof(int4) : 0},
-      {(void**)&dotp_, fuse_ && !xdot_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
-      {(void**)&dot_, fuse_ && !xdot_ ? Rp * 4 : 0},
+      {(void**)&dotp_, fuse_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
+      {(void**)&dot_, fuse_ ? Rp * 4 : 0},
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
       {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
       {&ws_.ptr, ws_.bytes},
@@ -245,7 +241,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
-    if (fuse_ && !xdot_) launch_dot_reduce(dotp_, dot_, g_, s);
+    if (fuse_) launch_dot_reduce(dotp_, dot_, g_, s);
   }
   if (zqt_pending_) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));

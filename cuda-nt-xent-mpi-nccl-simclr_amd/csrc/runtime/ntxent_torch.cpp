@@ -707,19 +707,17 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
                                  cpos.data_ptr<float>());
     return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
   }
-  // 16-bit plans finish the normalisation backward in the dZ epilogue: dot_i = z_i . g_i either
-  // from the dZ tiles themselves (dz_dot_exchange: one-round dZ launches) or from partials the
-  // coefficient pass emits (not on fp8-forward plans: that dot_i = sum_j C_ij cos_ij would use
-  // the e4m3 forward's cosines)
+  // 16-bit plans finish the normalisation backward in the dZ epilogue with dot_i = z_i . g_i =
+  // sum_j C_ij cos_ij from partials the coefficient pass emits (not on fp8-forward plans: that sum
+  // would use the e4m3 forward's cosines)
   const bool f8_fwd = cpos.numel() != P->g.rows_pad;  // see fused_forward
-  const bool xdot = dz_dot_exchange(P->g, P->bwd(), gemm_ws(h, P->n_dz, *P));
-  const bool fuse = P->bwd() != DType::F32 && P->g.dim % 8 == 0 && (!f8_fwd || xdot);
+  const bool fuse = P->bwd() != DType::F32 && P->g.dim % 8 == 0 && !f8_fwd;
   at::Tensor dotp, dot;
-  if (fuse && !xdot) {
+  if (fuse) {
     dotp = at::empty({(long)P->g.rows_pad * dot_slots(P->g)}, opts(h, at::kFloat));
     dot = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   }
-  float* dp = fuse && !xdot ? dotp.data_ptr<float>() : nullptr;
+  float* dp = fuse ? dotp.data_ptr<float>() : nullptr;
   at::Tensor cb;
   if (sc_in.has_value() && sc_in->defined()) {
     cb = coef(*sc_in, lse2, cpos, *P, dp);
@@ -729,13 +727,13 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   at::Tensor dh, go;
   NormFuse nf;
   if (fuse) {
-    if (!xdot) launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
+    launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
     go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
     dh = at::empty_like(h);
     nf.h = h.data_ptr();
     nf.in = to_dtype(h.scalar_type());
     nf.inv = inv.data_ptr<float>();
-    nf.dot = xdot ? nullptr : dot.data_ptr<float>();
+    nf.dot = dot.data_ptr<float>();
     nf.grad_out = go.data_ptr<float>();
     nf.dh = dh.data_ptr();
   }

@@ -8,9 +8,9 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4}; mkdir -p $OUT
 timeout -k 10 400 build/bin/ntxent_tests > $OUT/cpp_tests.log 2>&1 || { echo "cpp tests failed"; tail -30 $OUT/cpp_tests.log; exit 1; }
 tail -1 $OUT/cpp_tests.log
 if [ "$2" != "skip-tests" ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rA --durations 15 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?
-tail -3 $OUT/pytest_gpu.log
+grep -E "passed|failed" $OUT/pytest_gpu.log | tail -2
 grep -E "^(FAILED|ERROR)" $OUT/pytest_gpu.log | head -30
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest aborted rc=$rc"; exit 1; fi
 fi
