@@ -291,12 +291,6 @@ struct NormFuse {
 bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
                void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false,
                const NormFuse* nf = nullptr, const Q8Stats* q8 = nullptr, const float* cpos = nullptr);
-// The same dZ for 16-bit plans with B = the (gathered) rows Zq_all [W * rows_pad][ld_k] as the
-// prep wrote them: the GEMM reads Z through transposed LDS reads, so no ZqT copy is made.
-bool dz_rows_eligible(DType comp);
-bool launch_dz_rows(DType comp, const void* cbuf, const void* zq_all, const int4* tiles, int ntiles, void* dz,
-                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false,
-                    const NormFuse* nf = nullptr);
 
 // (A dZ that reads only the upper-triangular C, mirrored K-steps and Z through transposed LDS reads,
 // measured 33 us slower than the mirrored C + Z^T path at the headline: profiles/r3/dzexp.)

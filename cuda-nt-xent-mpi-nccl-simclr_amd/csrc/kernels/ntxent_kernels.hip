@@ -733,13 +733,6 @@ void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
 
 template <typename Tc, int MODE>
 void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
-  if constexpr (MODE == dev::kModeDz && sizeof(Tc) == 2) {
-    if (p.b_rows) {
-      hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, dev::kDzBRows>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
-      return;
-    }
-  }
-  NTXENT_CHECK(!p.b_rows, "sim_gemm: natural-row B needs a 16-bit dZ");
   if (MODE == dev::kModeFwd && !p.fixed_shift)
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, MODE == dev::kModeFwd ? 0 : 1>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
@@ -1329,27 +1322,9 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
   return true;
 }
 
-bool dz_rows_eligible(DType comp) { return comp == DType::F16 || comp == DType::BF16; }
-
-static bool dz_impl(DType comp, const void* sc, const void* zb, bool b_rows, const int4* tiles, int ntiles,
-                    void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
-                    const NormFuse* nf, const Q8Stats* q8, const float* cpos);
-
 bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
                void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
                const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
-  return dz_impl(comp, sc, zqt_all, false, tiles, ntiles, slabs, ws, g, stream, out_f16, nf, q8, cpos);
-}
-
-bool launch_dz_rows(DType comp, const void* sc, const void* zq_all, const int4* tiles, int ntiles, void* slabs,
-                    const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16, const NormFuse* nf) {
-  NTXENT_CHECK(dz_rows_eligible(comp), "dz_rows: 16-bit plans only");
-  return dz_impl(comp, sc, zq_all, true, tiles, ntiles, slabs, ws, g, stream, out_f16, nf, nullptr, nullptr);
-}
-
-static bool dz_impl(DType comp, const void* sc, const void* zb, bool b_rows, const int4* tiles, int ntiles,
-                    void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
-                    const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
   if (ntiles == 0) return false;
   const bool f8 = comp == DType::FP8;
   NTXENT_CHECK(!f8 || (q8 && q8->mneg2 && q8->lmin && q8->zq && cpos && g.world == 1 && out_f16),
@@ -1365,22 +1340,13 @@ static bool dz_impl(DType comp, const void* sc, const void* zb, bool b_rows, con
   }
   // A = C, tile-blocked (coef_tile_operand)
   p.A = coef_tile_operand(sc, g.col_tiles, cs);
-  p.B.base = static_cast<const char*>(zb);
-  if (b_rows) {
-    // B = Zq_all [W * rows_pad][ld_k] as stored: a K-step is 64 rows, a column tile 256 columns
-    p.b_rows = 1;
-    p.B.ld = (long long)g.ld_k * cs;
-    p.B.row_tile_stride = (long long)kTile * cs;
-    p.B.kblk = kKStepBytes;
-    p.B.kblk_stride = 64 * p.B.ld;
-  } else {
-    // B = ZqT_all [W][dim_n][ld_t]: rows = embedding dims, K = global columns, one K block per rank.
-    const long long ldt = f8 ? q8_ldt(g) : g.ld_t;
-    p.B.ld = ldt * cs;
-    p.B.row_tile_stride = (long long)kTile * ldt * cs;
-    p.B.kblk = (long long)g.rows_pad * cs;
-    p.B.kblk_stride = (long long)g.dim_n * ldt * cs;
-  }
+  // B = ZqT_all [W][dim_n][ld_t]: rows = embedding dims, K = global columns, one K block per rank.
+  p.B.base = static_cast<const char*>(zqt_all);
+  const long long ldt = f8 ? q8_ldt(g) : g.ld_t;
+  p.B.ld = ldt * cs;
+  p.B.row_tile_stride = (long long)kTile * ldt * cs;
+  p.B.kblk = (long long)g.rows_pad * cs;
+  p.B.kblk_stride = (long long)g.dim_n * ldt * cs;
   p.tiles = tiles;
   p.kbytes = (long long)g.world * g.rows_pad * cs;
   p.out = static_cast<float*>(slabs);

@@ -17,12 +17,6 @@
 // operands across whole-tile work items: the last two K-steps' prefetches load the next item's
 // first two, under the epilogue (see kStreamMode in the kernel).
 //
-// dZ with 16-bit operands reads B = Z in its natural row layout (K = rows j, N = embedding
-// columns): a half-tile is 64 rows x 128 columns, 256-byte LDS rows with 16-byte chunk ch of row
-// r at chunk ch ^ brow_swz(r), filled by the same lane-linear DMA (the swizzle goes on the source
-// address) and read as the MFMA's K-contiguous operand with ds_read_b64_tr_b16
-// (cdna_hip_programming.md T10, image (b)) -- no transposed copy of Zq.
-//
 // Accumulator acc[mi][ni] (mi < 8, ni < 4) covers tile rows rbase(mi)..+15 and columns
 // cbase(ni)..+15 with rbase(mi) = 128(mi>>2) + 64 wa + 16(mi&3), cbase(ni) = 128(ni>>1) +
 // 32 wb + 16(ni&1) for wave w = 4 wa + wb. Kept cosine tiles use a canonical fragment order
@@ -39,14 +33,6 @@ namespace ntxent {
 namespace dev {
 
 enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
-// sim_gemm_kernel's third template argument: the forward's exponential form (FX below), or for
-// the dZ which B operand layout it reads
-constexpr int kDzBTransposed = 1;  // B = Z^T rows (embedding dims), K-contiguous
-constexpr int kDzBRows = 2;        // B = Z rows, read transposed from LDS (16-bit types)
-
-// 16-byte chunk swizzle of a 256-byte natural-B LDS row: conflict-free ds_read_b64_tr_b16 for
-// the 16x16x32 operand (two 4-row blocks 8 rows apart per 32-lane half)
-__device__ __forceinline__ int brow_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
 constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 64 KiB
 // cache-policy bits of the GEMM operand LDS-DMA (0: default policy; experiment builds set
@@ -73,8 +59,7 @@ struct OperandDesc {
 };
 
 struct SimParams {
-  OperandDesc A, B;      // (dZ rows B: ld = row stride, row_tile_stride = 256 columns in bytes,
-                         //  kblk = 128, kblk_stride = 64 rows)
+  OperandDesc A, B;
   const int4* tiles;
   long long kbytes;      // K bytes handled by one workgroup
   int R, Rpad, n_half, own0, row_tile0, col_tiles;
@@ -97,7 +82,6 @@ struct SimParams {
   long long ldo;         // elements
   long long slab_stride; // elements
   int accum;             // dZ: add the tile into `out` (sub-block GEMMs of one gradient)
-  int b_rows;            // dZ: B is Z in natural rows (kDzBRows), else Z^T rows
   int out_f16;           // dZ: write `out` as fp16 (partner gradient contributions on the wire)
   // Fused normalisation backward (see dot_slots / dz_store):
   float* dotp;           // coefficient pass: partials of dot_i = sum_j C_ij cos_ij, [4 col_tiles][Rpad]
@@ -764,11 +748,8 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
 // ------------------------------------------------------------------------------------
 // FX: the forward epilogue's exponential form, fixed shift (1, tau > ~0.024) or per-tile max
 // (0). A compile-time choice: with both forms in one kernel the allocator spilled the main loop.
-// dZ: the B operand layout (kDzBTransposed, kDzBRows).
 template <typename T, int MODE, int FX = 1>
 __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams p) {
-  constexpr bool kBRows = MODE == kModeDz && FX == kDzBRows;
-  static_assert(!kBRows || sizeof(T) == 2, "natural-row B operand: 16-bit types only");
   typedef typename Mfma<T>::frag frag;
   typedef __attribute__((address_space(3))) const frag lds_frag;
   // fp8: 2 KiB more hold the dwords carrying the tile's 256 A-row and 256 B-row E8M0 scales (one
@@ -798,13 +779,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
       a_off[h][j] = (unsigned)(row * p.A.ld) + lchunk * 16;
       b_off[h][j] = (unsigned)(row * p.B.ld) + lchunk * 16;
-      if constexpr (kBRows) {
-        // natural B: the wave's piece j of half-tile h is LDS rows 4 (2w + j) .. + 3 (1 KiB, the
-        // same destination as above); lane -> row 4 (2w + j) + lane / 16, LDS chunk lane % 16,
-        // holding source chunk (lane % 16) ^ brow_swz(row) of the half's 128 columns
-        const int br = 4 * (2 * w + j) + (lane >> 4);
-        b_off[h][j] = (unsigned)(br * p.B.ld) + 256 * h + 16 * ((lane & 15) ^ brow_swz(br));
-      }
     }
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
@@ -852,29 +826,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   };
   auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
     const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
-    if constexpr (kBRows) {
-      // lane (r16, cq) needs B rows 32 s + 8 cq .. + 7 of column 32 wb + 16 ni + r16: two 4-row
-      // transposed reads; lane 4q + p of a 16-lane group addresses row q, columns 4p .. 4p + 3
-      typedef short v4s_ __attribute__((ext_vector_type(4)));
-      typedef __attribute__((address_space(3))) v4s_ lds_v4s;
-      const lds_char* Bh = Bs + h * kHalfBytes;
-      const int q = r16 >> 2, pp = r16 & 3;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int ch = ((32 * wb + 16 * ni) >> 3) + (pp >> 1);
-          union { v4s_ h[2]; frag f; } u;
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            const int row = 32 * s + 8 * cq + 4 * t + q;
-            u.h[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (lds_v4s*)(Bh + 256 * row + 16 * (ch ^ brow_swz(row)) + 8 * (pp & 1)));
-          }
-          bf[s][ni] = u.f;
-        }
-      return;
-    }
     i32x4 lo[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -937,12 +888,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     asm volatile("" ::: "memory");
   };
   auto lds_drain = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-  // phase 1 issues the 8 A0 reads before the 4 B0 reads (8 transposed ones for natural B); LDS
-  // reads retire in order
-  auto a0_retire = [&]() {
-    if constexpr (kBRows) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-  };
+  // phase 1 issues the 8 A0 reads before the 4 B0 reads; LDS reads retire in order
+  auto a0_retire = [&]() { asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); };
   // Forward streaming (MODE == kModeFwd, 16-bit operands, whole-tile items): the operand
   // streams run from one item into the next, so the schedule's trailing stages (K-steps n and
   // n + 1 of an n-step item: A0 B0 B1 A1, A0 B0 B1 — exactly a prologue) stage the NEXT item's

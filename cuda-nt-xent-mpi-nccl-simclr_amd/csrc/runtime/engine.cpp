@@ -53,8 +53,6 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   // the symmetric mode sums received contributions in launch_norm_bwd instead)
   // (not on fp8 plans: dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines, ~1e-2 off)
   fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && g_.dim % 8 == 0;
-  // (fp8-forward plans gather only the e4m3 rows: their fp16 rows stay rank-local)
-  rows_b_ = cfg.dz_rows && !small_ && !symm_ && !q8_ && dz_rows_eligible(bwd_) && !(f8_ && world_ > 1);
 
   const auto ft = symm_ ? build_sym_fwd_tiles(g_, jobs_, nch_) : build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -69,7 +67,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   const std::vector<Slot> slots = {
       {(void**)&zq_all_, W * Rp * g_.ld_k * cs_},
       {(void**)&zq8_all_, f8_ ? W * Rp * g_.ld_k8 : 0},
-      {(void**)&zqt_all_, q8_ || rows_b_ ? 0 : W * g_.dim_n * g_.ld_t * cs_},
+      {(void**)&zqt_all_, q8_ ? 0 : W * g_.dim_n * g_.ld_t * cs_},
       {(void**)&zq8t_, q8_ ? (size_t)g_.dim_n * (size_t)q8_ldt(g_) : 0},
       {(void**)&q8_mneg_, q8_ ? Rp * 4 : 0},
       {(void**)&q8_lmin_, q8_ ? (size_t)4 : (size_t)0},
@@ -165,7 +163,7 @@ void Engine::forward(const void* h, hipStream_t s) {
     }
     launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
     // world 1: the transpose is written by the LSE launch (beside the merge, see below)
-    if (world_ > 1 && !rows_b_) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
+    if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
@@ -173,11 +171,10 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_prep_, 0));
     comm_->all_gather(op_local, op_all, op_bytes, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_zq_, comm_stream_));
-    if (!rows_b_) {  // the backward's B operand: the ZqT blocks
-      comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
-      NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
-      zqt_pending_ = true;
-    }
+    // the backward's B operand: the ZqT blocks
+    comm_->all_gather(zqt_local, zqt_all_, (size_t)g_.dim_n * g_.ld_t * cs_, comm_stream_);
+    NTXENT_HIP_CHECK(hipEventRecord(ev_zqt_, comm_stream_));
+    zqt_pending_ = true;
   }
   // both forward launches overlap a gather (rows, then ZqT): leave CUs for the RCCL kernels
   GemmWorkspace ws_ovl = ws_;
@@ -203,7 +200,7 @@ void Engine::forward(const void* h, hipStream_t s) {
       q8.lmin = q8_lmin_;
       q8.zq8t = zq8t_;
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
-    } else if (world_ == 1 && !rows_b_)
+    } else if (world_ == 1)
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
     else
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
@@ -263,8 +260,6 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     const bool fused =
         q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
                         fuse_ ? &nf : nullptr, &q8, cpos_)
-        : rows_b_ ? launch_dz_rows(bwd_, cbuf_, zq_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
-                                   fuse_ ? &nf : nullptr)
             : launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32,
                         fuse_ ? &nf : nullptr);
     if (fused) return;  // dh written by the dZ epilogue
