@@ -144,10 +144,9 @@ void* upload(std::vector<float>& host, DType in) {
 class Bench {
  public:
   Bench(int batch, int dim, DType in, DType comp, float T, bool keep_cos, Comm* comm, unsigned seed,
-        bool small_path = true, int small_splits = 0, Negatives neg = Negatives::kSymmetric, bool prep_t = true)
+        bool small_path = true, int small_splits = 0, Negatives neg = Negatives::kSymmetric)
       : in_(in) {
     EngineConfig c;
-    c.fused_prologue = prep_t;
     c.negatives = neg;
     c.rows = 2 * batch;
     c.dim = dim;
@@ -293,7 +292,7 @@ struct Options {
   int batch = 0, dim = 0, iters = 100, warmup = 1, gpus = 1;
   std::string dtype = "bf16", compute = "auto", json;
   float T = 0.07f;
-  bool check = false, graph = false, recompute = false, small = true, grad_digest = false, prep_t = true;
+  bool check = false, graph = false, recompute = false, small = true, grad_digest = false;
   int small_splits = 0;
   Negatives negatives = Negatives::kSymmetric;
   bool emulate = false;  // --gpus N as N emulated ranks on GPU 0 (ThreadComm), not N GPUs over RCCL
@@ -346,7 +345,7 @@ int run_multi(const Options& o, DType in, DType comp) {
         std::unique_ptr<Comm> comm;
         if (o.emulate) comm = std::make_unique<ThreadComm>(group, r);
         else comm = std::make_unique<RcclComm>(r, N, uid, r);
-        Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, comm.get(), 1234 + r, true, 0, o.negatives, o.prep_t);
+        Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, comm.get(), 1234 + r, true, 0, o.negatives);
         bar.wait();
         const Result fb = stats(bench.time(o.graph ? 3 : 2, o.warmup, o.iters));
         mean_ms[r] = fb.mean;
@@ -395,7 +394,7 @@ int run_proc(const Options& o, DType in, DType comp) {
     NTXENT_CHECK(uid.size() == RcclComm::kIdBytes, "timed out waiting for the uid file");
   }
   RcclComm comm(r, N, uid, o.shared_gpu ? 0 : r);
-  Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, &comm, 1234 + r, true, 0, o.negatives, o.prep_t);
+  Bench bench(o.batch, o.dim, in, comp, o.T, !o.recompute, &comm, 1234 + r, true, 0, o.negatives);
   const Result fb = stats(bench.time(o.graph ? 3 : 2, o.warmup, o.iters));
   std::printf("proc rank %d/%d B/rank=%d D=%d %s %s: fwd+bwd %.4f ms, loss %.6f\n", r, N, o.batch, o.dim,
               o.dtype.c_str(), o.negatives == Negatives::kSymmetric ? "symmetric" : "allgather", fb.mean,
@@ -421,7 +420,6 @@ int main(int argc, char** argv) {
     else if (a == "--json") o.json = next();
     else if (a == "--check") o.check = true;
     else if (a == "--grad-digest") o.grad_digest = true;
-    else if (a == "--no-prep-t") o.prep_t = false;
     else if (a == "--graph") o.graph = true;
     else if (a == "--recompute") o.recompute = true;
     else if (a == "--no-small") o.small = false;
@@ -449,7 +447,6 @@ int main(int argc, char** argv) {
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --grad-digest: print a hash of dh after one step (build variants must match bitwise)\n"
-                  "  --no-prep-t: separate prep and transpose launches instead of the fused prologue\n"
                   "  (the measured A/B alternatives of earlier rounds are deleted; build-time variants:\n"
                   "   tools/build_variant.sh)\n");
       return 0;
@@ -483,8 +480,7 @@ int main(int argc, char** argv) {
   if (jf) std::fprintf(jf, "{\"device\": \"%s\", \"results\": {", di.arch.c_str());
   bool first = true;
   for (auto [b, d] : shapes) {
-    Bench bench(b, d, in, comp, o.T, !o.recompute, nullptr, 1234, o.small, o.small_splits, Negatives::kSymmetric,
-                o.prep_t);
+    Bench bench(b, d, in, comp, o.T, !o.recompute, nullptr, 1234, o.small, o.small_splits);
     const char* path = bench.engine().small() ? "small" : "large";
     const Result f = stats(bench.time(0, o.warmup, o.iters));
     const Result bw = stats(bench.time(1, o.warmup, o.iters));

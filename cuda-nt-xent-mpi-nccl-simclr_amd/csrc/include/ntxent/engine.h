@@ -59,9 +59,6 @@ struct EngineConfig {
   // world > 1: CUs the similarity GEMMs leave free while an overlapped all-gather is in flight
   // (the persistent GEMM would otherwise hold every CU and the RCCL kernels could not start)
   int comm_reserve_cus = 8;
-  // eligible 16-bit plans: one prologue pass writes the rows and Z^T (launch_prep_t); false = the
-  // separate prep + transpose launches (A/B and fallback)
-  bool fused_prologue = true;
   Negatives negatives = Negatives::kSymmetric;  // world > 1 (kSymmetric keeps cosines)
   int device = -1;            // -1: current device
 };
@@ -112,7 +109,6 @@ class Engine {
   int n_fwd_ = 0, n_own_ = 0, n_dz_ = 0;
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
-  bool prep_t_ = false;        // prep writes Z^T too (launch_prep_t), no transpose launch / blocks
   bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
   float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
   float* dot_ = nullptr;       // dot [Rpad]

@@ -166,12 +166,6 @@ size_t gemm_workspace_bytes(int ntiles, int num_cus);
 // ypos is then computed from the dequantised fp8 rows.
 void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, float* ypos,
                  const Geometry& g, hipStream_t stream, void* zq8 = nullptr);
-// launch_prep plus the dZ GEMM's B operand zqt = Zq^T ([dim_n][ld_t], rank-local rows) from the
-// same pass over h (16-bit plans, dim % 256 == 0, dim <= 2048, no pad rows: prep_t_eligible);
-// the LSE launch then runs without its transpose blocks.
-bool prep_t_eligible(DType comp, const Geometry& g);
-void launch_prep_t(DType in, DType comp, const void* h, void* zq, void* zqt, float* inv, float* ypos,
-                   const Geometry& g, hipStream_t stream);
 
 // out[i] = sum over k = 0 .. n-1 (in order) of in[k * count + i].
 void launch_sum_slabs(const float* in, int n, size_t count, float* out, hipStream_t stream);

@@ -415,100 +415,6 @@ __device__ __forceinline__ void transpose_tile_q8(const _Float16* __restrict__ z
   }
 }
 
-// Row prologue and the dZ GEMM's Z^T in one pass (16-bit plans, d <= 2048): h is read once.
-// A block normalises kPtPairs pairs (rows i0 .. i0 + 15 and their partners, one wave per two
-// pairs, rows in registers as in prep_wave_kernel), writes them to zq and to a [32][d] LDS image
-// (16-byte chunk c of row r at c ^ brow_swz(r) inside its 256-byte period), then writes Z^T columns
-// from that image: ds_read_b64_tr_b16 hands each lane 4 rows of one column, two reads = the 8
-// consecutive rows of one 16-byte Z^T store (cdna_hip_programming.md T10; conflict-free: the two
-// 4-row blocks of a 32-lane half are 8 rows apart). Replaces prep + the LSE launch's transpose
-// blocks: 96 instead of 128 MiB at the headline.
-constexpr int kPtPairs = 16;
-__device__ __forceinline__ int brow_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-template <typename Tin, typename Tc, int NCH>
-__global__ __launch_bounds__(512) void prep_t_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
-                                                     Tc* __restrict__ zqt, float* __restrict__ inv,
-                                                     float* __restrict__ ypos, int R, int d, int ldk, int ldt,
-                                                     float y_scale) {
-  static_assert(sizeof(Tc) == 2, "prep_t: 16-bit rows");
-  __shared__ __attribute__((aligned(16))) char img[2 * kPtPairs * 2048 * 2];
-  typedef __attribute__((address_space(3))) u32x4 lds_u4;
-  typedef short v4s __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) v4s lds_v4s;
-  lds_char* lds = (lds_char*)img;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int n = R >> 1, i0 = blockIdx.x * kPtPairs;
-  const int S = d * 2;  // image row stride (bytes; a multiple of 512)
-  auto phys = [&](int r, int c) { return r * S + 16 * ((c & ~15) | ((c & 15) ^ brow_swz(r))); };
-  float a[2][2][NCH][8];  // [pair][row i / p][chunk][8]
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const Tin* src = h + (long long)(i0 + 2 * w + q + v * n) * d;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int e = (c * 64 + lane) * 8;
-        if (e < d) load8<Tin>(src + e, a[q][v][c]);
-        else
-#pragma unroll
-          for (int j = 0; j < 8; ++j) a[q][v][c][j] = 0.f;
-      }
-    }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int i = i0 + 2 * w + q, pi = i + n;
-    float ss[2] = {0.f, 0.f};
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ss[v] += a[q][v][c][j] * a[q][v][c][j];
-    const float ivi = 1.0f / fmaxf(sqrtf(wave_sum(ss[0])), 1e-12f);
-    const float ivp = 1.0f / fmaxf(sqrtf(wave_sum(ss[1])), 1e-12f);
-    float dot = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int e = (c * 64 + lane) * 8;
-      if (e >= d) continue;
-      float qv[2][8];
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        union { u32x4 u; Tc x[8]; } pk;
-        const float iv = v ? ivp : ivi;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { pk.x[j] = from_f32<Tc>(a[q][v][c][j] * iv); qv[v][j] = to_f32<Tc>(pk.x[j]); }
-        *reinterpret_cast<u32x4*>(zq + (long long)(v ? pi : i) * ldk + e) = pk.u;
-        *(lds_u4*)(lds + phys(2 * w + q + 16 * v, e >> 3)) = pk.u;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dot += qv[0][j] * qv[1][j];
-    }
-    dot = wave_sum(dot);
-    if (lane == 0) {
-      inv[i] = ivi; inv[pi] = ivp;
-      ypos[i] = dot * y_scale; ypos[pi] = dot * y_scale;
-    }
-  }
-  // zq rows [d, ldk) are never read by the GEMMs (K = dim_k = d here)
-  __syncthreads();
-  // Z^T: wave w takes 16-column groups w, w + 8, ...; lane (g = lane / 16, i = lane % 16) stores
-  // rows 8g .. 8g + 7 of column e0 + i (g < 2: rows i0 + 8g.., else the partners n + i0 + 8(g-2)..)
-  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
-  const long long jb = g < 2 ? i0 + 8 * g : (long long)n + i0 + 8 * (g - 2);
-  for (int e0 = 16 * w; e0 < d; e0 += 16 * 8) {
-    union { v4s h[2]; u32x4 u; } o;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int r = 8 * g + 4 * t + qq;
-      const int col = e0 + 4 * pp;
-      o.h[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(lds + phys(r, col >> 3) + 2 * (col & 7)));
-    }
-    *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + li) * ldt + jb) = o.u;
-  }
-}
-
 // out[i] = sum_k in[k * count + i], k = 0 .. n-1 in order (deterministic reductions of the
 // in-process communicator).
 __global__ __launch_bounds__(256) void sum_slabs_kernel(const float* __restrict__ in, int n, size_t count,
@@ -1153,36 +1059,6 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
         hipLaunchKernelGGL((dev::prep_kernel<Tin, Tc, false>), dim3(g.rows / 2 + pad), dim3(256), 0, stream,
                            static_cast<const Tin*>(h), static_cast<Tc*>(zq), inv, ypos, g.rows, g.dim,
                            g.dim_k, g.ld_k, ys, nullptr, 0, 0);
-    });
-  });
-  NTXENT_HIP_CHECK(hipGetLastError());
-}
-
-bool prep_t_eligible(DType comp, const Geometry& g) {
-  return (comp == DType::F16 || comp == DType::BF16) && g.dim % 256 == 0 && g.dim <= 2048 && g.dim == g.dim_n &&
-         g.dim_k == g.dim && g.rows == g.rows_pad && (g.rows / 2) % dev::kPtPairs == 0;
-}
-
-void launch_prep_t(DType in, DType comp, const void* h, void* zq, void* zqt, float* inv, float* ypos,
-                   const Geometry& g, hipStream_t stream) {
-  NTXENT_CHECK(prep_t_eligible(comp, g), "prep_t: 16-bit plan, d % 256 == 0, d <= 2048, no pad rows");
-  const float ys = g.inv_temp * dev::kLog2e;
-  const int nch = (g.dim + 511) / 512;
-  const dim3 grid(g.rows / 2 / dev::kPtPairs);
-  dispatch_comp(in, [&](auto tin) {
-    using Tin = decltype(tin);
-    dispatch_comp(comp, [&](auto tc) {
-      using Tc = decltype(tc);
-      if constexpr (sizeof(Tc) == 2) {
-        auto go = [&](auto nc) {
-          constexpr int NC = decltype(nc)::value;
-          hipLaunchKernelGGL((dev::prep_t_kernel<Tin, Tc, NC>), grid, dim3(512), 0, stream, static_cast<const Tin*>(h),
-                             static_cast<Tc*>(zq), static_cast<Tc*>(zqt), inv, ypos, g.rows, g.dim, g.ld_k, g.ld_t, ys);
-        };
-        if (nch == 1) go(std::integral_constant<int, 1>{});
-        else if (nch == 2) go(std::integral_constant<int, 2>{});
-        else go(std::integral_constant<int, 4>{});
-      }
     });
   });
   NTXENT_HIP_CHECK(hipGetLastError());

@@ -53,7 +53,6 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
   // the symmetric mode sums received contributions in launch_norm_bwd instead)
   // (not on fp8 plans: dot_i = sum_j C_ij cos_ij would use the e4m3 forward's cosines, ~1e-2 off)
   fuse_ = !small_ && !symm_ && !f8_ && bwd_ != DType::F32 && g_.dim % 8 == 0;
-  prep_t_ = cfg.fused_prologue && !small_ && !symm_ && !f8_ && prep_t_eligible(bwd_, g_);
 
   const auto ft = symm_ ? build_sym_fwd_tiles(g_, jobs_, nch_) : build_fwd_tiles(g_);
   const auto dt = build_dz_tiles(g_);
@@ -162,13 +161,9 @@ void Engine::forward(const void* h, hipStream_t s) {
       if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
       return;
     }
-    if (prep_t_) {  // rows and Z^T from one pass over h
-      launch_prep_t(cfg_.input, bwd_, h, zq_local, zqt_local, inv_, ypos_, g_, s);
-    } else {
-      launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
-      // world 1: the transpose is written by the LSE launch (beside the merge, see below)
-      if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
-    }
+    launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
+    // world 1: the transpose is written by the LSE launch (beside the merge, see below)
+    if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
   if (world_ > 1) {
     // Gathers on the comm stream; the own-rank tiles only need this rank's slot.
@@ -205,7 +200,7 @@ void Engine::forward(const void* h, hipStream_t s) {
       q8.lmin = q8_lmin_;
       q8.zq8t = zq8t_;
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
-    } else if (world_ == 1 && !prep_t_)
+    } else if (world_ == 1)
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
     else
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);

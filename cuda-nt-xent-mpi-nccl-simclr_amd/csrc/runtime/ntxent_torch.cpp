@@ -199,21 +199,6 @@ std::vector<at::Tensor> prep(const at::Tensor& h, const Plan& P, const c10::opti
   return {zq, inv, ypos, zq8};
 }
 
-// prep + Z^T from one pass over h (prep_t_eligible plans): {zq, inv, ypos, zqt}
-std::vector<at::Tensor> prep_t(const at::Tensor& h, const Plan& P) {
-  check_input(h, "h");
-  NTXENT_CHECK(h.dim() == 2 && h.size(0) == P.g.rows && h.size(1) == P.g.dim, "h shape does not match plan");
-  NTXENT_CHECK(P.comp != DType::FP8 && prep_t_eligible(P.bwd(), P.g), "prep_t: plan not eligible");
-  const at::DeviceGuard guard(h.device());
-  auto zq = at::empty({P.g.rows_pad, P.g.ld_k}, opts(h, to_scalar(P.bwd())));
-  auto zqt = at::empty({P.g.dim_n, P.g.ld_t}, zq.options());
-  auto inv = at::empty({P.g.rows}, opts(h, at::kFloat));
-  auto ypos = at::empty({P.g.rows}, opts(h, at::kFloat));
-  launch_prep_t(to_dtype(h.scalar_type()), P.bwd(), h.data_ptr(), zq.data_ptr(), zqt.data_ptr(), inv.data_ptr<float>(),
-                ypos.data_ptr<float>(), P.g, cur_stream(h));
-  return {zq, inv, ypos, zqt};
-}
-
 at::Tensor transpose(const at::Tensor& zq, const Plan& P, const c10::optional<at::Tensor>& zqt_out) {
   check_input(zq, "zq");
   const at::DeviceGuard guard(zq.device());
@@ -632,16 +617,14 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
                      small_scratch(h, *P).data_ptr(), P->g, cur_stream(h));
     return {loss, zq, at::Tensor(), inv, lse2, at::Tensor(), arow};
   }
+  auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
+  // ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes it from
+  // extra blocks beside the merge (one stream: a side-stream transpose cost an event record and
+  // a join of ~5-7 us each, or stretched the forward GEMM when launched beside it).
+  auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
   // fp8 plans: the forward GEMM reads the e4m3 copy and always keeps its cosines (fp16), so
   // the fp16 backward uses exactly the forward's logits
   const bool f8 = comp == DType::FP8;
-  // ZqT (the dZ GEMM's B operand) is first read in the backward. 16-bit plans up to d = 2048 write
-  // it in the prep pass itself (h read once); otherwise the LSE launch writes it from extra blocks
-  // beside the merge (one stream: a side-stream transpose cost an event record and a join of
-  // ~5-7 us each, or stretched the forward GEMM when launched beside it).
-  const bool fused_t = !f8 && prep_t_eligible(P->bwd(), P->g);
-  auto pr = fused_t ? prep_t(h, *P) : prep(h, *P, c10::nullopt, c10::nullopt);
-  auto zqt = fused_t ? pr[3] : at::empty({P->g.dim_n, P->g.ld_t}, pr[0].options());
   auto fs = f8 ? fwd_stats(pr[3], pr[3], *P, true) : fwd_stats(pr[0], pr[0], *P, keep_cos);
   auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
   if (f8 && fp8_backward_enabled() && fp8_backward_eligible(P->g, comp)) {
@@ -663,7 +646,7 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
   }
   // (fp8 plans: 64 spare entries mark the e4m3 forward for the backward, which sees the fp16 rows)
   auto cpos = at::empty({P->g.rows_pad + (f8 ? 64 : 0)}, opts(h, at::kFloat));
-  auto loss = fused_t ? lse(fs[0], pr[2], lse2, cpos, *P) : lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
+  auto loss = lse(fs[0], pr[2], lse2, cpos, *P, pr[0], zqt);
   return {loss, pr[0], zqt, pr[1], lse2, fs[1], cpos};
 }
 
@@ -1079,8 +1062,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("prep", &prep, py::arg("h"), py::arg("plan"), py::arg("zq_out") = py::none(), py::arg("zq8_out") = py::none());
   m.def("transpose", &transpose, py::arg("zq"), py::arg("plan"), py::arg("zqt_out") = py::none());
-  m.def("prep_t_eligible", [](const Plan& P) { return P.comp != ntxent::DType::FP8 && ntxent::prep_t_eligible(P.bwd(), P.g); });
-  m.def("prep_t", &prep_t, py::arg("h"), py::arg("plan"));
   m.def("fwd_stats_range", &fwd_stats_range, py::arg("zq_local"), py::arg("zq_all"), py::arg("plan"), py::arg("part"),
         py::arg("sc"), py::arg("first"), py::arg("count"), py::arg("reserve_cus") = 0);
   m.def("fwd_stats", [](const at::Tensor& zl, const at::Tensor& za, const Plan& P, bool keep) {
