@@ -126,12 +126,10 @@ __device__ __forceinline__ int sc_unit(int rb, int cb, int lane) { return ((rb >
 struct KStream {
   const char* ptr;  // the K-step to stage next
   int kin, left;    // byte offset inside its K block; K-steps after it
-  int past;         // stages issued past the last K-step (the schedule's trailing prefetches)
   __device__ __forceinline__ void init(const char* base, long long k0, const OperandDesc& o, int nk) {
     kin = (int)(k0 % o.kblk);
     ptr = base + (k0 / o.kblk) * o.kblk_stride + kin;
     left = nk - 1;
-    past = 0;
   }
   __device__ __forceinline__ void advance(const OperandDesc& o) {
     if (left > 0) {
@@ -139,8 +137,6 @@ struct KStream {
       ptr += kKStepBytes;
       kin += kKStepBytes;
       if (kin == o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }
-    } else {
-      ++past;
     }
   }
 };
@@ -784,36 +780,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       a_off[h][j] = (unsigned)(row * p.A.ld) + lchunk * 16;
       b_off[h][j] = (unsigned)(row * p.B.ld) + lchunk * 16;
     }
-  // Fused dZ epilogue: the schedule's 7 trailing stages of a whole tile would re-load its last
-  // K-step (clamped streams) into buffers nobody reads again. They load the epilogue's rows of h
-  // instead (rows 2 P, 2 P + 1 of the tile per 1-KiB piece P, 16-bit h: 224 of 256 rows), so its
-  // h reads hit L2 rather than paying the memory latency once the MFMAs are done. Same DMA count
-  // per stage, so every counted wait is unchanged.
-#ifndef NTXENT_DZ_HPF
-#define NTXENT_DZ_HPF 1
-#endif
-  constexpr bool kHPf = NTXENT_DZ_HPF && MODE == kModeDz && !std::is_same<T, fp8e4m3>::value;
-  const char* hpf = nullptr;  // h tile of the current whole-tile dZ item (null: plain clamping)
-  int hrows = 0, hcols = 0, hst = 0;
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
-    if constexpr (kHPf) {
-      if (hpf != nullptr && s.past > 0) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int piece = (2 * hst + j) * 8 + w;
-          int row = 2 * piece + (lane >> 5);
-          row = row < hrows ? row : hrows - 1;
-          const int col = 8 * (lane & 31) < hcols ? 8 * (lane & 31) : 0;
-          __builtin_amdgcn_global_load_lds((const void*)(hpf + ((long long)row * p.nd + col) * 2),
-                                           (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, kGemmDmaAux);
-        }
-        ++hst;
-        s.advance(isB ? p.B : p.A);
-        return;
-      }
-    }
     const char* src = s.ptr;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -1000,16 +969,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(Ab, k0, p.A, ns); sa1.init(Ab, k0, p.A, ns);
     sb0.init(Bb, k0, p.B, ns); sb1.init(Bb, k0, p.B, ns);
-    if constexpr (kHPf) {
-      hpf = nullptr;
-      hst = 0;
-      if (p.ndh != nullptr && p.nh_dt != 0 && !p.splitk && ns == nk) {
-        hrows = p.R - tt.x * kTile < kTile ? p.R - tt.x * kTile : kTile;
-        hcols = p.nd - tt.y * kTile < kTile ? p.nd - tt.y * kTile : kTile;
-        if (hrows > 0 && hcols > 0)
-          hpf = static_cast<const char*>(p.nh) + ((long long)tt.x * kTile * p.nd + (long long)tt.y * kTile) * 2;
-      }
-    }
     if constexpr (kF8 && MODE != kModeDz) {
       // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
       // B row t - 256 (stored right after the row's K range) into smem[kScaleLds + 4 t] by a
