@@ -308,10 +308,12 @@ def run_rank(a) -> None:
             loss, gh = step()
             if evs:
                 evs[i + 1].record()
+        t_enq = time.perf_counter()  # host side done: the GPU may still be working
         sync()
         barrier()
         sync()
         dt = time.perf_counter() - t0
+        timed.host_ms = (t_enq - t0) / steps * 1e3
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else None
         comm_ms = None
         if comm:
@@ -350,6 +352,7 @@ def run_rank(a) -> None:
     # add several per step at N > 1): the per-step distribution and the per-rank communication
     # waits come from a separate pass right after it.
     dt_s, _, _, loss, gh = timed(step, a.steps, a.warmup, per_step_events=False, comm=False)
+    host_ms = timed.host_ms  # host CPU time to enqueue one step (autograd + launches) in the timed run
     per_ms = comm_ms = None
     if on_gpu or world > 1:
         _, per_ms, comm_ms, _, _ = timed(step, min(a.steps, 20), 0, per_step_events=on_gpu, comm=world > 1)
@@ -373,6 +376,7 @@ def run_rank(a) -> None:
         return [float(v) for v in t.cpu()]
 
     dt_s = rank_max(dt_s)
+    host_ms = rank_max(host_ms)
     ok = rank_max(0.0 if finite else 1.0) == 0.0
     ms = dt_s / a.steps * 1e3
     value = world * a.batch / (ms / 1e3)
@@ -442,6 +446,10 @@ def run_rank(a) -> None:
             "step_ms": _stats(per_ms) if per_ms else None,
             "step_ms_source": ("HIP events around each of %d steps, a separate pass after the timed region"
                                % min(a.steps, 20)) if per_ms else None,
+            "host_enqueue_ms_per_step": round(host_ms, 4),
+            "host_enqueue_note": ("host CPU time to issue one step (autograd graph + kernel launches) in the "
+                                  "timed run, max over ranks; the GPU is the bottleneck while it is below "
+                                  "ms_per_step"),
             "peak_hbm_mb": round(peak_mb, 1) if peak_mb is not None else None,
             "peak_hbm_mb_per_rank": [round(x, 1) for x in peak_all] if peak_all else None,
             "comm_wait_ms_per_step": {k: round(v, 4) for k, v in comm_ms.items()} if comm_ms else None,
