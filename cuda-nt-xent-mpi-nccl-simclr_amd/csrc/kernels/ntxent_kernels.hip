@@ -1131,9 +1131,6 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   p.kbytes = kb;
   p.part = part;
   p.sc = static_cast<char*>(sc);
-  // kept tiles beyond half the 256 MiB MALL: non-temporal stores (config 5, 260 MiB: coefficient
-  // pass -10 us, dZ -4 us; at 66 MiB the default policy is 4 us faster: profiles/r4/variants_r4_v2.md)
-  p.sc_nt = (long long)ntiles * kTileElems * (comp == DType::F32 ? 4 : 2) > (128ll << 20) ? 1 : 0;
   p.b_tile0 = bv.b_tile0;
   p.part_x = part_x;
   const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;

@@ -41,6 +41,12 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 6
 #define NTXENT_GEMM_DMA_AUX 0
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
+// 16-byte write-through (sc1) store at base + off: the line goes to memory at once, so the kernel
+// boundary has no dirty L2 lines of it to write back
+__device__ __forceinline__ void store16_wt(void* base, long long off, u32x4 v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(base) + (off & ~0xFFFFFFFll), 0, 0x7FFFFFFF, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(off & 0xFFFFFFFll), 0, 16);
+}
 // Byte offset of element (r, c) inside a row-major 256 x 256 coefficient tile of es-byte
 // elements. (A K-step-blocked layout, [kstep][row][128 B], measured neutral: profiles/r4/variants.)
 __device__ __forceinline__ long long ctile_off(int r, int c, int es) { return ((long long)r * kTile + c) * es; }
@@ -71,8 +77,6 @@ struct SimParams {
   int fixed_shift;       // 1: exponentials use the fixed shift M (2M < 120, see fwd epilogue)
   float2* part;          // [col_tiles][Rpad] partial (max, sum) in log2 units
   char* sc;              // kept cosines: [n_fwd_tiles][256*256] (canonical fragment order)
-  int sc_nt;             // 1: kept-cosine stores are non-temporal (set when the kept tiles exceed
-                         //    half the MALL: they are re-read only by the coefficient pass)
   char* cbuf;            // coefficients: [row_tiles][col_tiles][256*256] (row-major per tile)
   const float* lse2;     // [W*Rpad] lse in log2 units (all ranks)
   const float* cpos;     // [Rpad] positive coefficient C_i,p(i) = -(a_i + a_p), a = 1 - P_ip
@@ -1118,9 +1122,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
             pk.h[r] = from_f32<TS>(acc[mi][2 * np][r]);
             pk.h[4 + r] = from_f32<TS>(acc[mi][2 * np + 1][r]);
           }
-          u32x4* dst = reinterpret_cast<u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8);
-          if (p.sc_nt) __builtin_nontemporal_store(pk.u, dst);
-          else *dst = pk.u;
+          // write-through: -1.1 % headline, -2.3 % config 2 fwd+bwd vs default-policy stores, config
+          // 5 as the non-temporal form (profiles/r4/variants_r4_v7_wt.md)
+          store16_wt(st, (long long)sc_unit(rb[mi], cb[2 * np], lane) * 16, pk.u);
         } else {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
