@@ -45,6 +45,12 @@ template <typename T> __device__ __forceinline__ void load8_h(const T* p, float 
 template <> __device__ __forceinline__ void load8<_Float16>(const _Float16* p, float (&v)[8]) { load8_h(p, v); }
 template <> __device__ __forceinline__ void load8<__bf16>(const __bf16* p, float (&v)[8]) { load8_h(p, v); }
 
+#ifndef NTXENT_ZQ_WT
+#define NTXENT_ZQ_WT 0
+#endif
+#ifndef NTXENT_ZQT_WT
+#define NTXENT_ZQT_WT 0
+#endif
 template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8], float (&q)[8]) {
   if constexpr (sizeof(T) == 2) {
     union { uint4 u; T h[8]; } pk;
@@ -56,6 +62,19 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
     for (int j = 0; j < 8; ++j) q[j] = v[j];
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
     *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+
+// store8 into base[off .. off + 7] (base uniform: one buffer resource, per-lane offsets); zq rows
+// write-through under NTXENT_ZQ_WT
+template <typename T> __device__ __forceinline__ void store8_at(T* base, long long off, const float (&v)[8], float (&q)[8]) {
+  if constexpr (sizeof(T) == 2 && NTXENT_ZQ_WT) {
+    union { u32x4 u; T h[8]; } pk;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { pk.h[j] = from_f32<T>(v[j]); q[j] = to_f32<T>(pk.h[j]); }
+    store16_wt(base, off * 2, pk.u);
+  } else {
+    store8<T>(base + off, v, q);
   }
 }
 
@@ -254,8 +273,8 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
       float qa[8], qb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { a[c][j] *= ivi; b[c][j] *= ivp; }
-      store8<Tc>(zi + e, a[c], qa);
-      store8<Tc>(zp + e, b[c], qb);
+      store8_at<Tc>(zq, (long long)i * ldk + e, a[c], qa);
+      store8_at<Tc>(zq, (long long)pi * ldk + e, b[c], qb);
       if constexpr (Q8) {
         *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa, sci);
         *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb, scp);
@@ -334,8 +353,8 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
       float qa[8], qb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) { a[c][j] *= ivi; b[c][j] *= ivp; }
-      store8<Tc>(zi + e, a[c], qa);
-      store8<Tc>(zp + e, b[c], qb);
+      store8_at<Tc>(zq, (long long)i * ldk + e, a[c], qa);
+      store8_at<Tc>(zq, (long long)pi * ldk + e, b[c], qb);
       if constexpr (Q8) {
         *reinterpret_cast<u32x2*>(zq8 + (long long)i * ldk8 + e) = quant8(a[c], qa, sci);
         *reinterpret_cast<u32x2*>(zq8 + (long long)pi * ldk8 + e) = quant8(b[c], qb, scp);
@@ -382,7 +401,8 @@ __device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __re
     union { T h[V]; u32x4 u; } pk;
 #pragma unroll
     for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][((er / V) ^ (jc % CPR)) * V + er % V];
-    *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
+    if constexpr (NTXENT_ZQT_WT) store16_wt(zqt, ((long long)(e0 + er) * ldt + j0 + jc * V) * (long long)sizeof(T), pk.u);
+    else *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
   }
 }
 

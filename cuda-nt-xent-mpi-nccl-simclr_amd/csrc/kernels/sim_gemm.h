@@ -705,12 +705,12 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
           union { __bf16 h[8]; u32x4 u; } y;
 #pragma unroll
           for (int e = 0; e < 8; ++e) y.h[e] = (__bf16)o[e];
-          *reinterpret_cast<u32x4*>(static_cast<__bf16*>(p.ndh) + off) = y.u;
+          store16_wt(p.ndh, off * 2, y.u);  // write-through (profiles/r4/variants_r4_v8_wt.md)
         } else if (p.nh_dt == 1) {
           union { _Float16 h[8]; u32x4 u; } y;
 #pragma unroll
           for (int e = 0; e < 8; ++e) y.h[e] = (_Float16)o[e];
-          *reinterpret_cast<u32x4*>(static_cast<_Float16*>(p.ndh) + off) = y.u;
+          store16_wt(p.ndh, off * 2, y.u);
         } else {
           f32x4* op = reinterpret_cast<f32x4*>(static_cast<float*>(p.ndh) + off);
           op[0] = f32x4{o[0], o[1], o[2], o[3]};
