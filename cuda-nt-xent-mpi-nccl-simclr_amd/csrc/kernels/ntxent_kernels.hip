@@ -45,12 +45,6 @@ template <typename T> __device__ __forceinline__ void load8_h(const T* p, float 
 template <> __device__ __forceinline__ void load8<_Float16>(const _Float16* p, float (&v)[8]) { load8_h(p, v); }
 template <> __device__ __forceinline__ void load8<__bf16>(const __bf16* p, float (&v)[8]) { load8_h(p, v); }
 
-#ifndef NTXENT_ZQ_WT
-#define NTXENT_ZQ_WT 0
-#endif
-#ifndef NTXENT_ZQT_WT
-#define NTXENT_ZQT_WT 0
-#endif
 template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8], float (&q)[8]) {
   if constexpr (sizeof(T) == 2) {
     union { uint4 u; T h[8]; } pk;
@@ -65,10 +59,10 @@ template <typename T> __device__ __forceinline__ void store8(T* p, const float (
   }
 }
 
-// store8 into base[off .. off + 7] (base uniform: one buffer resource, per-lane offsets); zq rows
-// write-through under NTXENT_ZQ_WT
+// store8 into base[off .. off + 7], 16-bit rows write-through (sc1; base uniform: one buffer
+// resource, per-lane offsets): prep -1 us at every BASELINE shape (profiles/r4/variants_r4_v9_wt.md)
 template <typename T> __device__ __forceinline__ void store8_at(T* base, long long off, const float (&v)[8], float (&q)[8]) {
-  if constexpr (sizeof(T) == 2 && NTXENT_ZQ_WT) {
+  if constexpr (sizeof(T) == 2) {
     union { u32x4 u; T h[8]; } pk;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { pk.h[j] = from_f32<T>(v[j]); q[j] = to_f32<T>(pk.h[j]); }
@@ -401,8 +395,7 @@ __device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __re
     union { T h[V]; u32x4 u; } pk;
 #pragma unroll
     for (int q = 0; q < V; ++q) pk.h[q] = tile[jc * V + q][((er / V) ^ (jc % CPR)) * V + er % V];
-    if constexpr (NTXENT_ZQT_WT) store16_wt(zqt, ((long long)(e0 + er) * ldt + j0 + jc * V) * (long long)sizeof(T), pk.u);
-    else *reinterpret_cast<u32x4*>(zqt + (long long)(e0 + er) * ldt + j0 + jc * V) = pk.u;
+    store16_wt(zqt, ((long long)(e0 + er) * ldt + j0 + jc * V) * (long long)sizeof(T), pk.u);  // write-through
   }
 }
 
