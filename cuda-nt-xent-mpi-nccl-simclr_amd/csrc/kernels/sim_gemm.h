@@ -47,15 +47,7 @@ __device__ __forceinline__ void store16_wt(void* base, long long off, u32x4 v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(base) + (off & ~0xFFFFFFFll), 0, 0x7FFFFFFF, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(off & 0xFFFFFFFll), 0, 16);
 }
-__device__ __forceinline__ void store8_wt(void* base, long long off, u32x2 v) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(base) + (off & ~0xFFFFFFFll), 0, 0x7FFFFFFF, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b64(v, rs, (int)(off & 0xFFFFFFFll), 0, 16);
-}
-// write-through for the diagonal remainder's and split-K reduce's kept cosines and the split-K dZ
-// reduce's dh (experiment switch NTXENT_WT2)
-#ifndef NTXENT_WT2
-#define NTXENT_WT2 0
-#endif
+
 // Byte offset of element (r, c) inside a row-major 256 x 256 coefficient tile of es-byte
 // elements. (A K-step-blocked layout, [kstep][row][128 B], measured neutral: profiles/r4/variants.)
 __device__ __forceinline__ long long ctile_off(int r, int c, int es) { return ((long long)r * kTile + c) * es; }
@@ -1528,8 +1520,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
           pk.h[r] = from_f32<TS>(acc[2 * h2][r]);
           pk.h[4 + r] = from_f32<TS>(acc[2 * h2 + 1][r]);
         }
-        if constexpr (NTXENT_WT2) store16_wt(sto, (long long)sc_unit(rb0, 64 * b + 32 * h2, lane) * 16, pk.u);
-        else *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * h2, lane) * 8) = pk.u;
+        *reinterpret_cast<u32x4*>(sto + sc_unit(rb0, 64 * b + 32 * h2, lane) * 8) = pk.u;
       }
     } else {
 #pragma unroll
@@ -1731,8 +1722,7 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
           pk.h[r] = from_f32<TS>(v[2 * np][r]);
           pk.h[4 + r] = from_f32<TS>(v[2 * np + 1][r]);
         }
-        if constexpr (NTXENT_WT2) store16_wt(st, (long long)sc_unit(s16, 64 * w + 32 * np, lane) * 16, pk.u);
-        else *reinterpret_cast<u32x4*>(st + sc_unit(s16, 64 * w + 32 * np, lane) * 8) = pk.u;
+        *reinterpret_cast<u32x4*>(st + sc_unit(s16, 64 * w + 32 * np, lane) * 8) = pk.u;
       }
     } else {
 #pragma unroll
@@ -1864,8 +1854,7 @@ __global__ __launch_bounds__(256) void sk_dz_reduce_kernel(const SimParams p) {
           if (p.nh_dt == 1) y.f[r] = (_Float16)o[r];
           else y.b[r] = (__bf16)o[r];
         }
-        if constexpr (NTXENT_WT2) store8_wt(p.ndh, off * 2, y.u);
-        else *reinterpret_cast<u32x2*>(static_cast<char*>(p.ndh) + off * 2) = y.u;
+        *reinterpret_cast<u32x2*>(static_cast<char*>(p.ndh) + off * 2) = y.u;
       }
     } else if (p.out_f16) {
       union { _Float16 h[4]; u32x2 u; } pk;
