@@ -1365,12 +1365,9 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
 // Ring of the diagonal-remainder kernel below: a stage holds 64 A + 64 B rows of one K-step.
 constexpr int kSubStage = 128 * kKStepBytes;   // 16 KiB
 // ring stages of the diagonal remainder's off-diagonal-region blocks (diagonal-region blocks: twice
-// as many half-size stages); experiment switch NTXENT_UP_STAGES (3 or 6)
-#ifndef NTXENT_UP_STAGES
-#define NTXENT_UP_STAGES 3
-#endif
-constexpr int kSubStages = NTXENT_UP_STAGES;
-static_assert(kSubStages == 3 || kSubStages == 6, "diag_up ring: 3 or 6 stages");
+// as many half-size stages; 6 measured the same at the headline, +8 us at config 5:
+// profiles/r4/variants_r4_v11_up6.md)
+constexpr int kSubStages = 3;
 
 // ------------------------------------------------------------------------------------
 // Diagonal tiles by their upper 64x64 regions only (the coefficient pass mirrors a diagonal
@@ -1452,14 +1449,9 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
     // own pieces of step st landed (the P - 1 younger steps' np each in flight: 2 x 4 or 4 x 1);
     // after the barrier every wave's have, and every wave has finished reading the buffer
     // refilled next (the one read in the previous step)
-    // (P - 1) younger steps of np pieces each: 3 stages 4 x 2 / 1 x 4, 6 stages 10 x 2 / 4 x 4
-    if constexpr (kSubStages == 3) {
-      if (dg) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      if (dg) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    }
+    static_assert(kSubStages == 3, "wait counts assume 6- and 3-stage rings");
+    if (dg) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     const int nb2 = buf == 0 ? NSt - 1 : buf - 1;  // (st + P) % NSt
     stage(st + P < k1 ? st + P : k1 - 1, nb2);
