@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--T", type=float, default=0.07)
+    ap.add_argument("--modes", default="allgather,symmetric", help="subset of allgather,symmetric")
     a = ap.parse_args()
 
     from ntxent_amd.ops import _ext
@@ -97,6 +98,7 @@ def main():
 
             row = {"W": W, "rank": r, "batch": a.batch, "dim": d}
             modes = [("allgather", allgather_step)] + ([("symmetric", symmetric_step)] if W > 1 else [])
+            modes = [m for m in modes if m[0] in a.modes.split(",")]
             for name, fn in modes:
                 for _ in range(2):
                     fn()
@@ -108,7 +110,7 @@ def main():
                 e1.record()
                 e1.synchronize()
                 row[name + "_ms"] = round(e0.elapsed_time(e1) / a.iters, 4)
-            if W > 1:
+            if "allgather_ms" in row and "symmetric_ms" in row:
                 row["speedup"] = round(row["allgather_ms"] / row["symmetric_ms"], 3)
             print(json.dumps(row), flush=True)
             results.append(row)
