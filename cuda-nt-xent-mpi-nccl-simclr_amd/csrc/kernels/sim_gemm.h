@@ -41,11 +41,6 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 6
 #define NTXENT_GEMM_DMA_AUX 0
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
-// once-read loads (kept cosines in the coefficient pass, h in the fused dZ epilogue) non-temporal:
-// experiment switch NTXENT_NT_LD
-#ifndef NTXENT_NT_LD
-#define NTXENT_NT_LD 0
-#endif
 // 16-byte write-through (sc1) store at base + off: the line goes to memory at once, so the kernel
 // boundary has no dirty L2 lines of it to write back
 __device__ __forceinline__ void store16_wt(void* base, long long off, u32x4 v) {
@@ -660,9 +655,9 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
       for (int k = 0; k < 16; ++k) {
         const int idx = tid + kGemmThreads * k, rt = idx >> 5, c = idx & 31;
         const int m = mt * kTile + rt, d0 = nt * kTile + 8 * c;
-        const u32x4* hp = reinterpret_cast<const u32x4*>(static_cast<const char*>(p.nh) + ((long long)m * p.nd + d0) * 2);
-        if constexpr (NTXENT_NT_LD) hq[k] = (m < p.R && d0 < p.nd) ? __builtin_nontemporal_load(hp) : u32x4{0u, 0u, 0u, 0u};
-        else hq[k] = (m < p.R && d0 < p.nd) ? *hp : u32x4{0u, 0u, 0u, 0u};
+        hq[k] = (m < p.R && d0 < p.nd)
+                    ? *reinterpret_cast<const u32x4*>(static_cast<const char*>(p.nh) + ((long long)m * p.nd + d0) * 2)
+                    : u32x4{0u, 0u, 0u, 0u};
       }
     }
     __syncthreads();
@@ -1350,8 +1345,9 @@ __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
     for (int np = 0; np < 2; ++np) {
       if constexpr (sizeof(T) == 2) {
         union { T h[8]; u32x4 u; } pk;
-        if constexpr (NTXENT_NT_LD) pk.u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8));
-        else pk.u = *reinterpret_cast<const u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8);
+        // read once: non-temporal (config 5 coefficient pass -8 us, headline -1 us:
+        // profiles/r4/variants_r4_v12_ntld.md)
+        pk.u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(st + sc_unit(rb[mi], cb[2 * np], lane) * 8));
         acc[mi][2 * np] = f32x4{to_f32<T>(pk.h[0]), to_f32<T>(pk.h[1]), to_f32<T>(pk.h[2]), to_f32<T>(pk.h[3])};
         acc[mi][2 * np + 1] = f32x4{to_f32<T>(pk.h[4]), to_f32<T>(pk.h[5]), to_f32<T>(pk.h[6]), to_f32<T>(pk.h[7])};
       } else {
