@@ -688,8 +688,8 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
 }
 
 // dot_i = sum over the coefficient pass's slots dotp[k][i] (slot-major; fixed order: deterministic).
-// 4 threads per row (slots q, q + 4, ...; 8 loads in flight each), 64 rows per block: the loads
-// of a wave cover 16 consecutive rows of 4 slots.
+// 4 threads per row (slots q, q + 4, ...; 32 or 8 loads in flight each, summed in slot order),
+// 64 rows per block: the loads of a wave cover 16 consecutive rows of 4 slots.
 __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict__ dotp, int nslot, int rows,
                                                          float* __restrict__ dot) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
@@ -697,6 +697,13 @@ __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict
   float s = 0.f;
   if (i < rows) {
     int k = q;
+    for (; k + 124 < nslot; k += 128) {  // 32 loads in flight (config 5, 256 slots: 8.0 -> 6.1 us)
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = dotp[(long long)(k + 4 * u) * rows + i];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) s += v[u];
+    }
     for (; k + 28 < nslot; k += 32) {
       float v[8];
 #pragma unroll

@@ -9,11 +9,15 @@ B = 4096/view, d = 2048) on two 512-tile lists with the same instruction stream:
   same512  512 copies of tile (0, 1): every CU of an XCD streams the same two panels in near
            lockstep, so all but the first touch of a line is an L2 hit
 
+  zero512  the plan's tiles on all-zero operands: same instructions and addresses, near-zero
+           switching energy in the MFMAs, so a clock the chip holds down under load rises
+           (MI355X_MICROARCH.md, DVFS give-back)
+
 If same512 is much faster, the loop pays for the L2 misses' latency and a prefetch path that
 does not take the CU's L1 request slots (e.g. another kernel's loads on the same XCD) could buy
 the difference. If it is not, the L2 miss rate is not what holds the loop.
 
-usage: tools/l2_bound_probe.py [--only plan512|same512] [--iters N]
+usage: tools/l2_bound_probe.py [--only plan512|same512|zero512] [--iters N]
 """
 import argparse
 import sys
@@ -28,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=None)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warm", type=int, default=400)
     args = ap.parse_args()
     from ntxent_amd.ops import _ext
     C = _ext.load(build_if_missing=False)
@@ -39,25 +44,28 @@ def main():
     zq, inv, ypos, _ = C.prep(h, plan)
     part = torch.empty((plan.col_tiles, plan.rows_pad, 2), dtype=torch.float32, device=dev)
     t = plan.fwd_tiles.cpu()
-    lists = {"plan512": t[:512].clone(), "same512": t[:1].repeat(512, 1)}
+    lists = {"plan512": t[:512].clone(), "same512": t[:1].repeat(512, 1), "zero512": t[:512].clone()}
+    zq0 = torch.zeros_like(zq)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for name, lst in lists.items():
         if args.only and name != args.only:
             continue
         td = lst.contiguous().to(dev)
-        for _ in range(3):
-            C.fwd_stats_tiles(zq, zq, 0, td, plan, part)
+        op = zq0 if name == "zero512" else zq  # zero512: the plan's tiles on all-zero operands
+        for _ in range(args.warm):  # back to back: the clock settles under sustained load
+            C.fwd_stats_tiles(op, op, 0, td, plan, part)
         torch.cuda.synchronize()
         ts = []
-        for _ in range(args.iters):
+        for _ in range(args.iters):  # batches of 50 back-to-back launches
             ev[0].record()
-            C.fwd_stats_tiles(zq, zq, 0, td, plan, part)
+            for _ in range(50):
+                C.fwd_stats_tiles(op, op, 0, td, plan, part)
             ev[1].record()
             torch.cuda.synchronize()
-            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+            ts.append(ev[0].elapsed_time(ev[1]) * 1e3 / 50)
         ts.sort()
-        print(f"{name:8s} first tile {tuple(lst[0].tolist())} median {ts[len(ts) // 2]:.1f} us  "
-              f"min {ts[0]:.1f} us", flush=True)
+        print(f"{name:8s} first tile {tuple(lst[0].tolist())} per launch: median {ts[len(ts) // 2]:.1f} us  "
+              f"min {ts[0]:.1f} us (batches of 50 after {args.warm} warm launches)", flush=True)
 
 
 if __name__ == "__main__":
