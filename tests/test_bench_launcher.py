@@ -62,6 +62,9 @@ def test_single_rank_cpu_json_contract():
         assert k in d
     assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+    # host CPU time to issue one step (verdict r3: the wall-vs-event gap), measured in the timed run
+    assert 0.0 < d["host_enqueue_ms_per_step"] and d["host_enqueue_note"]
+    assert d["value"] == pytest.approx(16 / (d["ms_per_step"] / 1e3), rel=1e-3)
 
 
 def test_scaling_driver_cpu():
