@@ -767,7 +767,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the wave index as a scalar: the stage's LDS destinations (M0) stay scalar arithmetic instead
+  // of a VALU add + v_readfirstlane per DMA piece (main loop 39 -> 22 VALU per K-step and wave;
+  // headline dZ -2 %, forward -1.8 %, config 2 -4 %: profiles/r4/variants_r4_v18_wsgpr.md)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wa = w >> 2, wb = w & 3;
   const int G = gridDim.x;
   const int bid = xcd_remap(blockIdx.x, G);  // persistent block id (XCD-contiguous runs)
@@ -788,11 +791,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
-    const char* src = s.ptr;
+    // buffer_load ... lds from a scalar V# at the stream's K-step + the lane's 32-bit offset: no
+    // 64-bit VALU address add per piece as global_load_lds needs (main loop 22 -> 14 VALU per
+    // K-step and wave; headline dZ -2.9 %, forward -2.6 %: profiles/r4/variants_r4_v20_bufdma.md)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(s.ptr), 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src + (isB ? b_off[h][j] : a_off[h][j])),
-                                       (lds_void*)(dst + 8 * j * kKStepBytes), 16, 0, kGemmDmaAux);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8 * j * kKStepBytes), 16,
+                                               isB ? b_off[h][j] : a_off[h][j], 0, 0, kGemmDmaAux);
     s.advance(isB ? p.B : p.A);
   };
 
@@ -1017,8 +1023,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
   if (grp == 1) barrier();  // stagger group 1 by one barrier
-  for (int ks = 0; ks < nsteps; ++ks) {
-    const int cur = ks & 1, nxt = cur ^ 1;
+  // K-steps in pairs: the buffer parity is a compile-time constant in each copy, so the LDS
+  // read addresses are loop-invariant registers + immediates (headline dZ -1.9 %, forward -1.5 %,
+  // config 5 dZ -3.4 %: profiles/r4/variants_r4_v21_unroll2.md)
+  auto kstep = [&](const int ks, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
     if constexpr (kStreamMode) {
       // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
       if (cont && ks == nsteps - 2) {
@@ -1048,7 +1057,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     stage(1, 1, sb1, cur);          //   B1 of step ks+2
     barrier();                      // phase 4 C
     mma_quadrant(kI1, kI1, af, bf1);
+  };
+  int ks2 = 0;
+  for (; ks2 + 1 < nsteps; ks2 += 2) {
+    kstep(ks2, kI0);
+    kstep(ks2 + 1, kI1);
   }
+  if (ks2 < nsteps) kstep(ks2, kI0);
   if (grp == 0) barrier();  // re-align the groups
   if (kStreamMode && cont) {
     // the trailing stages are the next item's K-steps 0 and 1 (buffers of parity nk): leave
@@ -1399,7 +1414,8 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   typedef __attribute__((address_space(3))) const frag lds_frag;
   __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   lds_char* lds = (lds_char*)smem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // scalar wave index (scalar M0 arithmetic for the DMA pieces, as sim_gemm_kernel: -0.3 us)
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int KSD = KS / 2 > 1 ? KS / 2 : 1;        // K pieces of a diagonal region
   constexpr int NB = diag_up_blocks<KS>();            // blocks per tile
   const int nt_d = gridDim.x / NB;                    // diagonal tiles in this launch

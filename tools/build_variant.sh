@@ -7,5 +7,6 @@ cd "$(dirname "$0")/.."
 HIPCC=/opt/rocm/bin/hipcc
 INC=cuda-nt-xent-mpi-nccl-simclr_amd/csrc/include
 $HIPCC --offload-arch=gfx950 -std=c++17 -fPIC -I$INC -O3 "$@" -c cuda-nt-xent-mpi-nccl-simclr_amd/csrc/kernels/ntxent_kernels.hip -o build/ntxent_kernels_$TAG.o
-$HIPCC --offload-arch=gfx950 build/ntxent_bench.o build/ntxent_kernels_$TAG.o build/small_kernels.o build/engine.o build/engine_sym.o build/rccl_comm.o build/trace.o -o build/bin/ntxent_bench_$TAG -L/opt/rocm/lib -lrccl -ldl -Wl,-rpath,/opt/rocm/lib
+$HIPCC --offload-arch=gfx950 -std=c++17 -fPIC -I$INC -O3 "$@" -c cuda-nt-xent-mpi-nccl-simclr_amd/csrc/kernels/small_kernels.hip -o build/small_kernels_$TAG.o
+$HIPCC --offload-arch=gfx950 build/ntxent_bench.o build/ntxent_kernels_$TAG.o build/small_kernels_$TAG.o build/engine.o build/engine_sym.o build/rccl_comm.o build/trace.o -o build/bin/ntxent_bench_$TAG -L/opt/rocm/lib -lrccl -ldl -Wl,-rpath,/opt/rocm/lib
 echo built build/bin/ntxent_bench_$TAG
