@@ -3,10 +3,12 @@
 //   out tile (256 x 256) = A_tile (256 x K) * B_tile (256 x K)^T, both operands K-contiguous.
 //
 // Workgroup = 8 wave64s. K advances in 128-byte steps (64 fp16/bf16 or 32 fp32 per row).
-// LDS holds two K-steps (even/odd buffer) of A and B, each split into two 128-row halves
-// (A0, A1, B0, B1: 16 KiB each), filled by global_load_lds_dwordx4 (lane-linear
-// destination; the bank swizzle phys_chunk = chunk ^ ((row>>1)&7) is applied on the source
-// address and on the ds_read_b128 side, conflict-free for the 16x16x32 operand lane groups).
+// LDS holds two K-steps (even/odd buffer) of A and B, laid out [A even | A odd | B even |
+// B odd] (32 KiB each, so every operand read is a lane base + a 16-bit immediate), each split
+// into two 128-row halves (A0, A1, B0, B1: 16 KiB each), filled by buffer_load_dwordx4 ... lds
+// from a scalar V# (lane-linear destination; the bank swizzle phys_chunk = chunk ^ ((row>>1)&7)
+// is applied on the source offset and on the ds_read_b128 side, conflict-free for the 16x16x32
+// operand lane groups).
 //
 // Main loop: every K-step is 4 phases, one per 128x128 C-quadrant (A0B0, A0B1, A1B0, A1B1);
 // in each phase all 8 waves compute 64x32 of that quadrant (16 MFMA 16x16x32 per wave). A
@@ -34,7 +36,7 @@ namespace dev {
 
 enum SimMode : int { kModeFwd = 0, kModeCoef = 1, kModeDz = 2 };
 
-constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // A + B of one K-step = 64 KiB
+constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // one operand, both parities = 64 KiB
 // cache-policy bits of the GEMM operand LDS-DMA (0: default policy; experiment builds set
 // NTXENT_GEMM_DMA_AUX, e.g. 2 = nt, 1 = sc0: tools/build_variant.sh)
 #ifndef NTXENT_GEMM_DMA_AUX
@@ -51,7 +53,7 @@ __device__ __forceinline__ void store16_wt(void* base, long long off, u32x4 v) {
 // Byte offset of element (r, c) inside a row-major 256 x 256 coefficient tile of es-byte
 // elements. (A K-step-blocked layout, [kstep][row][128 B], measured neutral: profiles/r4/variants.)
 __device__ __forceinline__ long long ctile_off(int r, int c, int es) { return ((long long)r * kTile + c) * es; }
-constexpr int kGemmLds = 2 * kStageBytes;             // even/odd K-step = 128 KiB
+constexpr int kGemmLds = 2 * kStageBytes;             // A and B, even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
 constexpr int kCoefWaveLds = 64 * (64 * 2 + 16);      // 9 KiB: C^T of one 64x64 region
@@ -790,7 +792,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
-    lds_char* dst = lds + buf * kStageBytes + isB * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
+    // LDS layout [A even | A odd | B even | B odd] (32 KiB each): every operand read of either
+    // parity is its lane base + a 16-bit immediate (headline dZ -2.1 %: variants_r4_v23_ldsab.md)
+    lds_char* dst = lds + isB * kStageBytes + buf * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
     // buffer_load ... lds from a scalar V# at the stream's K-step + the lane's 32-bit offset: no
     // 64-bit VALU address add per piece as global_load_lds needs (main loop 22 -> 14 VALU per
     // K-step and wave; headline dZ -2.9 %, forward -2.6 %: profiles/r4/variants_r4_v20_bufdma.md)
@@ -817,7 +821,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   typedef __attribute__((address_space(3))) const i32x4 lds_i4;
   OP af[NS][4], bf0[NS][2], bf1[NS][2];
   auto read_a = [&](int buf, int h, OP (&af)[NS][4]) {
-    const lds_char* As = lds + buf * kStageBytes;
+    const lds_char* As = lds + buf * (kTile * kKStepBytes);
     i32x4 lo[4];  // fp8: k-substep 0, joined with substep 1 into a fully (re)defined operand (a
                   // .lo/.hi partial write would keep the other half live across the whole kernel)
 #pragma unroll
@@ -836,7 +840,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   };
   auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
-    const lds_char* Bs = lds + buf * kStageBytes + kTile * kKStepBytes;
+    const lds_char* Bs = lds + kStageBytes + buf * (kTile * kKStepBytes);
     i32x4 lo[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
