@@ -194,6 +194,14 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   // slot-major ([slot][Rpad]: a store instruction's lanes hold neighbouring rows)
   const int wq = NW == 8 ? ((threadIdx.x >> 6) & 3) : (col_base >> 6);  // column quarter of this wave
   float cdot[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // plain region (uniform): no self or positive element and no padding among this call's rows x
+  // columns, so C is the exponential alone, without the per-element compares and selects
+  // (coefficient pass -10 % at the headline and config 2: profiles/r4/variants_r4_v25_coefplain.md)
+  const int r_lo = mt * kTile + row_base, r_hi = r_lo + NROWS;
+  const int c_lo = nt * kTile + col_base, c_hi = c_lo + NCOLS;
+  auto hits = [&](int a0) { return a0 < c_hi && c_lo < a0 + NROWS; };
+  const bool plain = fixed && r_hi <= p.R && col_local0 + col_base + NCOLS <= p.R && !hits(p.own0 + r_lo) &&
+                     !hits(p.own0 + r_lo + p.n_half) && !hits(p.own0 + r_lo - p.n_half);
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
@@ -201,6 +209,14 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
     const int gi0 = mt * kTile + row_t0;  // 4 consecutive rows
     const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
     const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
+    if (plain) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float lrow = fast_exp2(M - lrow4[r]);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) c[ni][r] = fast_exp2(acc[mi][ni][r] * p.acc_scale - M) * (lrow + lcol[ni]);
+      }
+    } else
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int gi = gi0 + r;
