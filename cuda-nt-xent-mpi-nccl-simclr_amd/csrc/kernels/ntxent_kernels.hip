@@ -1120,9 +1120,12 @@ bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
 int q8_ldt(const Geometry& g) { return g.rows_pad; }
 
-// K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel; 4 pieces measured
-// +6 us at config 5, neutral at the headline: profiles/r4/variants_r4_v2.md)
-constexpr int kDiagKS = 2;
+// K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel): 2 from 32 K-steps
+// up (the headline: 1 piece +2 us), 1 below (config 2 -1.5 us, config 5 -0.4 us:
+// profiles/r4/variants_r4_v29_diagks1.md; 4 pieces measured +6 us at config 5,
+// profiles/r4/variants_r4_v2.md)
+constexpr int kDiagKS = 2;  // the most pieces any shape uses (workspace sizing)
+static int diag_ks(int nk_tile) { return nk_tile >= 32 ? 2 : 1; }
 
 // K pieces per tile of the split-K forward (0: not used): own-block launches with fewer tiles
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
@@ -1215,9 +1218,15 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // row-group partials in the column-partial area of the workspace
         float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                     (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
-        const dim3 sg(nstrip * dev::diag_up_blocks<kDiagKS>());
-        if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, kDiagKS>), sg, dim3(256), 0, stream, q, scratch);
-        else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, kDiagKS>), sg, dim3(256), 0, stream, q, scratch);
+        if (diag_ks(nk_tile) == 2) {
+          const dim3 sg(nstrip * dev::diag_up_blocks<2>());
+          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q, scratch);
+          else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2>), sg, dim3(256), 0, stream, q, scratch);
+        } else {
+          const dim3 sg(nstrip * dev::diag_up_blocks<1>());
+          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1>), sg, dim3(256), 0, stream, q, scratch);
+          else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1>), sg, dim3(256), 0, stream, q, scratch);
+        }
       }
     }
   });
