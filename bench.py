@@ -23,6 +23,7 @@ fewer GPUs than asked).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -88,6 +89,8 @@ def parse(argv=None):
                          "at steps 10-19, 0.44 from step 60 on: profiles/r2/ramp); reported in the JSON")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="launcher: seconds before the whole job is killed; ranks: process-group timeout")
+    ap.add_argument("--gc-pause", default="on", choices=["on", "off"],
+                    help="pause Python's cyclic GC inside the timed bracket (as timeit does; off: leave it running)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -268,6 +271,7 @@ def run_rank(a) -> None:
             kw = dict(dtype=hd.dtype, compute=compute, negatives=a.negatives, keep_cos=not a.recompute)
             eng = (NativeNTXent.from_process_group(R, a.dim, a.temperature, **kw) if world > 1
                    else NativeNTXent(R, a.dim, a.temperature, **kw))
+            make_step.engine_bytes = eng.device_bytes  # its own hipMalloc arena (not torch's allocator)
             return lambda: eng.step(hd)
 
         def step():
@@ -292,9 +296,16 @@ def run_rank(a) -> None:
 
     def timed(step, steps, warmup, per_step_events=True, comm=False):
         """warmup untimed steps, then exactly `steps` steps bracketed by barrier + synchronize
-        on both sides; returns (total s, per-step ms list or None, comm ms per step or None)."""
+        on both sides; returns (total s, per-step ms list or None, comm ms per step or None).
+        Python's cyclic garbage collector is paused inside the bracket (as ``timeit`` does): a
+        collection pause while the GPU queue is shallow, right after the synchronize, idles the
+        GPU for a whole step (BENCH_r04's event pass: one 0.72 ms step among 0.40 ms ones)."""
         for _ in range(warmup):
             loss, gh = step()
+        gc_was = gc.isenabled() and a.gc_pause == "on"
+        if gc_was:
+            gc.collect()
+            gc.disable()
         sync()
         barrier()
         sync()
@@ -313,6 +324,8 @@ def run_rank(a) -> None:
         barrier()
         sync()
         dt = time.perf_counter() - t0
+        if gc_was:
+            gc.enable()
         timed.host_ms = (t_enq - t0) / steps * 1e3
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else None
         comm_ms = None
@@ -355,8 +368,10 @@ def run_rank(a) -> None:
     host_ms = timed.host_ms  # host CPU time to enqueue one step (autograd + launches) in the timed run
     per_ms = comm_ms = None
     if on_gpu or world > 1:
-        _, per_ms, comm_ms, _, _ = timed(step, min(a.steps, 20), 0, per_step_events=on_gpu, comm=world > 1)
-    peak_mb = torch.cuda.max_memory_allocated(dev) / 2**20 if on_gpu else None
+        _, per_ms, comm_ms, _, _ = timed(step, min(a.steps, 20), 1, per_step_events=on_gpu, comm=world > 1)
+    # torch allocator peak, plus the native Engine's own arena (allocated once, outside torch)
+    peak_mb = ((torch.cuda.max_memory_allocated(dev) + getattr(make_step, "engine_bytes", 0)) / 2**20
+               if on_gpu else None)
     lossv = float(loss.item())
     finite = bool(lossv == lossv and torch.isfinite(gh).all().item())
 
@@ -444,9 +459,11 @@ def run_rank(a) -> None:
                              "~60 steps after a cold start (profiles/r2/ramp); the timed region is the "
                              "steady state") if prewarm else None,
             "step_ms": _stats(per_ms) if per_ms else None,
-            "step_ms_source": ("HIP events around each of %d steps, a separate pass after the timed region"
-                               % min(a.steps, 20)) if per_ms else None,
+            "step_ms_list": [round(x, 4) for x in per_ms] if per_ms else None,
+            "step_ms_source": ("HIP events around each of %d steps, a separate pass after the timed region "
+                               "(one untimed step first)" % min(a.steps, 20)) if per_ms else None,
             "host_enqueue_ms_per_step": round(host_ms, 4),
+            "gc_paused_in_timed_region": a.gc_pause == "on",
             "host_enqueue_note": ("host CPU time to issue one step (autograd graph + kernel launches) in the "
                                   "timed run, max over ranks; the GPU is the bottleneck while it is below "
                                   "ms_per_step"),

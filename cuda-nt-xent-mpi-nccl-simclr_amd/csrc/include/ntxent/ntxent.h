@@ -120,6 +120,11 @@ std::vector<int4> build_sym_fwd_tiles(const Geometry& g, const std::vector<SymJo
 std::vector<SymJob> sym_jobs(int world, int rank, int row_tiles);
 std::vector<SymJob> sym_incoming(int world, int rank, int row_tiles);
 int sym_num_chunks(int row_tiles);
+// Symmetric mode's compact coefficient buffer: a rank writes only the column blocks at distance
+// 0 .. W/2 from itself (its own block, the full partner blocks, the split block), so cbuf holds
+// [row_tiles][sym_c_ld(g)] tiles with global column tile nt at column slot (nt - rank * row_tiles)
+// mod col_tiles: min(W, W/2 + 1) blocks instead of W (5 of 8 at W = 8).
+int sym_c_ld(const Geometry& g);
 
 // Forward tiles (ti, tj_global, kind, 0). Own-rank block: upper triangle only, listed
 // first (count_own_fwd_tiles of them) so they can run while the remote rows are gathered; its
@@ -205,6 +210,10 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
 // pieces of every tile publish partial slabs and a second launch sums them and runs the
 // epilogue in strips; fwd_splitk_pieces = pieces per tile (0: the stream-K schedule).
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail);
+// Diagonal-remainder tiles of a launch (0: none, the stream-K schedule splits the remainder):
+// the tiles left after whole rounds on `cus` CUs when they are all diagonal tiles (ntiles % cus
+// <= diag_tail), for 2-byte / fp32 plans with >= 4 K-steps per tile.
+int fwd_diag_remainder(int ntiles, int nk_tile, int cus, int diag_tail, bool f8);
 // Small-problem path (on by default; off = the large-problem pipeline for every shape) and its
 // backward column splits (0 = small_bwd_splits). Test hooks: process-wide.
 void set_small_path(bool on);
@@ -247,7 +256,8 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 // Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
 // `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;
 // upper-triangular tiles of the own-rank block are mirrored; the positive entry is cpos[i].
-// mbuf (symmetric mode): mirrored coefficient tiles of kTileCross tiles, [slots][row_tiles][row_tiles]
+// mbuf (symmetric mode): cbuf is the compact [row_tiles][sym_c_ld(g)] layout (see sym_c_ld), and
+// the mirrored coefficient tiles of kTileCross tiles go to mbuf, [slots][row_tiles][row_tiles]
 // tiles with slot = (q - rank - 1) mod W (partners rank+1, rank+2, ... in order): tile (mt, nt)
 // lands transposed at mbuf tile (slot, nt % row_tiles, mt), i.e. the block C_{q,rank} that
 // multiplies this rank's rows in rank q's gradient; consecutive slots stack into one tall A.

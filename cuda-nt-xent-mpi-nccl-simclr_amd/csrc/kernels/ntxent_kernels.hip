@@ -781,7 +781,12 @@ dev::SimParams base_params(const Geometry& g) {
 // the head of the workspace are zero when it is allocated and every launch leaves them zero
 // (the last arriver of a tile resets its counter), so no memset node is needed per launch.
 // Returns the grid.
-size_t sk_counter_bytes(int num_cus) { return ((size_t)2 * std::max(1, num_cus) * 4 + 255) / 256 * 256; }
+// Counter region: 2 per CU for the stream-K tiles, and 14 per diagonal-remainder tile
+// (diag_up_kernel: 4 row-group + 10 region tickets) for up to num_cus - 1 remainder tiles.
+constexpr int kDiagTickets = 14;
+size_t sk_counter_bytes(int num_cus) {
+  return ((size_t)std::max(2, kDiagTickets) * std::max(1, num_cus) * 4 + 255) / 256 * 256;
+}
 
 int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipStream_t stream) {
   NTXENT_CHECK(p.kbytes % kKStepBytes == 0, "K not aligned to the K step");
@@ -969,6 +974,7 @@ std::vector<SymJob> sym_incoming(int world, int rank, int row_tiles) {
 }
 
 int sym_num_chunks(int row_tiles) { return std::max(1, std::min(4, row_tiles)); }
+int sym_c_ld(const Geometry& g) { return std::min(g.world, g.world / 2 + 1) * g.row_tiles; }
 
 GemmSchedule make_schedule(int ntiles, int nk, int num_cus) {
   // Whole tiles in data-parallel rounds of G = num_cus blocks; only the remainder tiles
@@ -1131,6 +1137,12 @@ static int diag_ks(int nk_tile) { return nk_tile >= 32 ? 2 : 1; }
 // than CUs and long K, where the stream-K schedule's last-arriving block would read p - 1
 // partial slabs serially (BASELINE config 4: 36 tiles x 128 K-steps, fixup ~40 % of the GEMM).
 
+int fwd_diag_remainder(int ntiles, int nk_tile, int cus, int diag_tail, bool f8) {
+  if (diag_tail <= 0 || f8 || nk_tile < 4 || cus <= 0) return 0;
+  const int q = ntiles / cus, rem = ntiles % cus;
+  return (q >= 1 && rem > 0 && rem <= diag_tail) ? rem : 0;
+}
+
 int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
   if (diag_tail <= 0 || ntiles <= 0 || ntiles >= cus || nk < 32) return 0;
   const int pcs = std::min(cus / ntiles, nk / 8);
@@ -1163,15 +1175,14 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   // coefficient pass mirrors the rest) instead of a third round / stream-K split: 528 forward
   // tiles at B = 4096/view are 2 rounds + 16 diagonal tiles. fp8 launches and short K (< 4
   // K-steps: no K halves) keep the stream-K split of the remainder.
-  int nstrip = 0;
-  if (diag_tail > 0 && !f8 && nk_tile >= 4) {
-    const int q = ntiles / std::max(1, cus), rem = ntiles % std::max(1, cus);
-    // 14 arrival tickets per tile in the counter region, 10 KS piece partials per tile in the
-    // slab region (diag_up_kernel)
-    if (q >= 1 && rem > 0 && rem <= diag_tail && 14 * rem <= 2 * ws.num_cus &&
-        (size_t)10 * kDiagKS * rem * 4096 <= (size_t)2 * ws.num_cus * kTileElems)
-      nstrip = rem;
-  }
+  const int nstrip = fwd_diag_remainder(ntiles, nk_tile, cus, diag_tail, f8);
+  // kDiagTickets arrival tickets per tile in the counter region (sized for any remainder below
+  // num_cus), 10 KS piece partials per tile in the slab region and 4 x 256 row-group partials per
+  // tile in the column-partial area (diag_up_kernel): every remainder of a whole-round launch fits
+  NTXENT_CHECK((size_t)kDiagTickets * nstrip * 4 <= sk_counter_bytes(ws.num_cus) &&
+                   (size_t)10 * kDiagKS * nstrip * 4096 <= (size_t)2 * ws.num_cus * kTileElems &&
+                   (size_t)nstrip * 4 * 64 * 4 <= (size_t)ws.num_cus * dev::kSkColpTile,
+               "diagonal remainder: workspace too small");
   const int nmain = ntiles - nstrip;
   const int pieces = part_x == nullptr ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
   int grid;
@@ -1209,6 +1220,8 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
     if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
       if (nstrip > 0) {
+        // (a plain, short-lived grid: it does not keep ws.sched_cus CUs free; a transfer in flight
+        // gets CUs back as its blocks retire within the ~15 us launch)
         NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diagonal remainder: row-major operands only");
         dev::SimParams q = p;
         q.tiles = tiles + nmain;
@@ -1305,6 +1318,10 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
   p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
   p.cbuf = static_cast<char*>(cbuf);
   p.mbuf = static_cast<char*>(mbuf);
+  if (mbuf != nullptr) {  // symmetric mode: compact cbuf (sym_c_ld)
+    p.c_ld = sym_c_ld(g);
+    p.c_rot = 1;
+  }
   p.lse2 = lse2_all;
   p.cpos = cpos;
   if (q8) {

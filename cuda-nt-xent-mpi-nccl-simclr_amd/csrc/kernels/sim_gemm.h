@@ -44,10 +44,18 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // one operand, both parit
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
 // 16-byte write-through (sc1) store at base + off: the line goes to memory at once, so the kernel
-// boundary has no dirty L2 lines of it to write back
+// boundary has no dirty L2 lines of it to write back. The buffer descriptor must be wave-uniform
+// (a per-lane one makes hipcc emit a waterfall loop): its base is the first active lane's offset
+// less 64 MiB, 1 MiB aligned (SGPR arithmetic), so any lane within 64 MiB below and ~1.9 GiB above
+// the first lane's offset stores at a non-negative 32-bit offset from it; callers' waves span a
+// few rows of one tensor (at most a few MiB).
 __device__ __forceinline__ void store16_wt(void* base, long long off, u32x4 v) {
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(base) + (off & ~0xFFFFFFFll), 0, 0x7FFFFFFF, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(off & 0xFFFFFFFll), 0, 16);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)off);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)off >> 32));
+  const long long f0 = (long long)(((unsigned long long)hi << 32) | lo) - (64ll << 20);
+  const long long wb = f0 > 0 ? (f0 & ~0xFFFFFll) : 0;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(static_cast<char*>(base) + wb, 0, 0x7FFFFFFF, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(off - wb), 0, 16);
 }
 
 // Byte offset of element (r, c) inside a row-major 256 x 256 coefficient tile of es-byte
@@ -56,7 +64,7 @@ __device__ __forceinline__ long long ctile_off(int r, int c, int es) { return ((
 constexpr int kGemmLds = 2 * kStageBytes;             // A and B, even/odd K-step = 128 KiB
 constexpr int kCtStride = kTile * 2 + 16;             // C^T staging row: 512 B + 16 B pad
 constexpr int kCoefLds = kTile * kCtStride;           // 132 KiB
-constexpr int kCoefWaveLds = 64 * (64 * 2 + 16);      // 9 KiB: C^T of one 64x64 region
+constexpr int kCoefWaveLds = 64 * (64 * 2 + 16);      // C^T of one 64x64 region (8 KiB used when swizzled: ct_swz)
 constexpr int kHalfBytes = 128 * kKStepBytes;         // one half-tile of one operand = 16 KiB
 
 struct OperandDesc {
@@ -74,6 +82,7 @@ struct SimParams {
   int R, Rpad, n_half, own0, row_tile0, col_tiles;
   int b_tile0;           // B operand: global column tile of the chunk's first row tile (ring mode)
   int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
+  int c_rot;             // symmetric mode: column slot (nt - row_tile0) mod col_tiles instead (sym_c_ld)
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
   float acc_scale;       // logit (log2 units) per accumulator unit (y_scale)
   int scale_off;         // fp8 operands: byte offset of each row's E8M0 scale (= K bytes of a row)
@@ -148,6 +157,25 @@ struct KStream {
   }
 };
 
+// C^T staging of one 64x64 region by one wave (coef_kernel): LDS row L (C column L) is 128 B of
+// 16 8-byte granules (4 C rows each); granule j sits at slot j ^ ct_swz(L). This is conflict-free
+// for all three accesses of the staging (MI355X_MICROARCH.md §LDS banking): the ds_write_b64 of a
+// fragment (16 lanes = 16 rows L of one granule, banks mod 32: the low 4 bits of L -> 16 distinct
+// slots), the ds_read_b64_tr_b16 row reads (32 lanes = rows {b..b+3, b+8..b+11} x 4 granules,
+// banks mod 64: slots' top 2 bits biject (L bit 1, L bit 3)) and the mirror's ds_read_b64 pairs
+// (rows L, L+2 of one row parity x 8 granules of one parity: slot bit 0 flips with L bit 1). The
+// round-4 form (rows padded to 144 B) was 2-way conflicted on all three (1.58 M conflict cycles
+// per headline coefficient pass, profiles/r4/pmc_final).
+__device__ __forceinline__ int ct_swz(int L) {
+  return ((L >> 1) & 1) | ((L & 1) << 1) | (((L >> 3) & 1) << 2) | ((((L >> 1) ^ (L >> 2)) & 1) << 3);
+}
+
+// Tile index of coefficient tile (mt, nt) in cbuf (row-major [row_tiles][c_ld] tiles).
+__device__ __forceinline__ long long ctile_index(const SimParams& p, int mt, int nt) {
+  const int cs = p.c_rot ? (nt - p.row_tile0 + p.col_tiles) % p.col_tiles : nt - p.c_tile0;
+  return (long long)mt * p.c_ld + cs;
+}
+
 // ------------------------------------------------------------------------------------
 // Coefficient epilogue shared by the store-mode coef kernel (NW = 1: one wave, a 128x64
 // region at (row_base, col_base)) and the recompute GEMM (NW = 8: the whole tile).
@@ -161,7 +189,16 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
                                               lds_char* lds, const SimParams& p, int lane) {
   constexpr int NROWS = NW == 8 ? kTile : NMI * 16;
   constexpr int NCOLS = NW == 8 ? kTile : 64;
-  constexpr int S = NROWS * 2 + 16;  // LDS row stride (bytes) of the C^T staging tile
+  // C^T staging: one wave (64 x 64 region): 128-B rows, granules swizzled by ct_swz; the whole
+  // tile (NW = 8, recompute path): rows padded by 16 B
+#ifndef NTXENT_COEF_SWZ
+#define NTXENT_COEF_SWZ 1  // A/B switch (tools/build_variant.sh -DNTXENT_COEF_SWZ=0: the round-4 padded rows)
+#endif
+  constexpr bool SWZ = NW == 1 && NTXENT_COEF_SWZ;
+  static_assert(!SWZ || (NROWS == 64 && NCOLS == 64), "swizzled C^T staging is for 64 x 64 regions");
+  constexpr int S = SWZ ? 128 : NROWS * 2 + 16;  // LDS row stride (bytes) of the C^T staging tile
+  // byte offset of C rows e .. e+3 (e % 4 == 0) of staged column L
+  auto ct_at = [&](int L, int e) { return SWZ ? L * S + (((e >> 2) ^ ct_swz(L)) << 3) : L * S + e * 2; };
   constexpr int NT = NW * 64;        // threads in the calling block
   T* base = reinterpret_cast<T*>(p.cbuf);
   const int col_local0 = (nt * kTile) % p.Rpad;  // rank-local column of this tile's col 0
@@ -180,10 +217,10 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
     lcol[ni] = fixed ? fast_exp2(M - l) : l;
     cvalid[ni] = (col_local0 + col_t) < p.R;
   }
-  T* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
+  T* slot = base + ctile_index(p, mt, nt) * kTileElems;
   T* mirror = nullptr;
   if (kind == kTileSymOff || kind == kTileDiagUp)  // (kTileDiagUp: the same tile's slot)
-    mirror = base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems;
+    mirror = base + ctile_index(p, nt - p.row_tile0, p.row_tile0 + mt) * kTileElems;
   else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
     const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
     const int slot = (q - p.row_tile0 / rt - 1 + W) % W;  // partners r+1, r+2, ... -> slots 0, 1, ...
@@ -260,8 +297,8 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         union { T h[4]; u32x2 u; } pk;
 #pragma unroll
         for (int r = 0; r < 4; ++r) pk.h[r] = from_f32<T>(c[ni][r]);
-        *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(lds + (col_t - col_base) * S +
-                                                                     (row_t0 - row_base) * 2) = pk.u;
+        *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(lds + ct_at(col_t - col_base, row_t0 - row_base)) =
+            pk.u;
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -296,7 +333,14 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       for (int q = 0; q < NCOLS * CPR / NT; ++q) {
         const int k = tid + NT * q;
         const int row = k / CPR, c16 = k % CPR;
-        const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
+        u32x4 v;
+        if constexpr (SWZ) {  // two 8-byte granules (not adjacent once swizzled)
+          typedef __attribute__((address_space(3))) const u32x2 lds_u2;
+          const u32x2 lo = *(lds_u2*)(lds + ct_at(row, 8 * c16)), hi = *(lds_u2*)(lds + ct_at(row, 8 * c16 + 4));
+          v = u32x4{lo[0], lo[1], hi[0], hi[1]};
+        } else {
+          v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(lds + row * S + c16 * 16);
+        }
         *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(mirror) + ctile_off(col_base + row, row_base + 8 * c16, 2)) = v;
       }
     }
@@ -312,9 +356,10 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       const int blk = w * NBLK + b;
       const int c0 = (blk % RB) * 16;  // C rows row_base+c0 .. +15
       const int r0 = (blk / RB) * 32 + 8 * g;  // C cols col_base+r0 .. +7
-      const lds_char* a0 = lds + (r0 + q4) * S + (c0 + 4 * p4) * 2;
+      const lds_char* a0 = lds + ct_at(r0 + q4, c0 + 4 * p4);
+      const lds_char* a1 = lds + ct_at(r0 + q4 + 4, c0 + 4 * p4);
       const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a0);
-      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(a0 + 4 * S));
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)a1);
       u32x4 u;
       u[0] = (unsigned short)lo[0] | ((unsigned)(unsigned short)lo[1] << 16);
       u[1] = (unsigned short)lo[2] | ((unsigned)(unsigned short)lo[3] << 16);
@@ -357,9 +402,9 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   lds_char* ld_d = lds;             // stored tile: [64 rows][64 cols]
   lds_char* ld_m = lds + 64 * S8;   // mirror: [64 cols][64 rows]
   unsigned char* base = reinterpret_cast<unsigned char*>(p.cbuf);
-  unsigned char* slot = base + ((long long)mt * p.c_ld + nt - p.c_tile0) * kTileElems;
+  unsigned char* slot = base + ctile_index(p, mt, nt) * kTileElems;
   unsigned char* mirror = (kind == kTileSymOff || kind == kTileDiagUp)
-                              ? base + ((long long)(nt - p.row_tile0) * p.c_ld + p.row_tile0 + mt - p.c_tile0) * kTileElems
+                              ? base + ctile_index(p, nt - p.row_tile0, p.row_tile0 + mt) * kTileElems
                               : nullptr;
   const int col_local0 = (nt * kTile) % p.Rpad;
   const bool fixed = p.fixed_shift != 0;

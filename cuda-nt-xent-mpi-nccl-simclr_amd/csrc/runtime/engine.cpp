@@ -75,7 +75,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&ypos_, R * 4},
       {(void**)&part_, (size_t)g_.col_tiles * Rp * sizeof(float2)},
       {(void**)&sbuf_, cfg_.keep_cos ? (size_t)n_fwd_ * kTileElems * cs_ : 0},
-      {(void**)&cbuf_, (size_t)g_.row_tiles * g_.col_tiles * kTileElems * cs_},
+      {(void**)&cbuf_, (size_t)g_.row_tiles * (symm_ ? sym_c_ld(g_) : g_.col_tiles) * kTileElems * cs_},
       {(void**)&lse2_all_, W * Rp * 4},
       {(void**)&cpos_, Rp * 4},
       {(void**)&block_loss_, (size_t)lse_scratch_floats(g_) * 4},

@@ -184,7 +184,7 @@ void Engine::forward_sym(const void* h, hipStream_t s) {
 
 void Engine::backward_sym(const float* grad_out, void* dh, hipStream_t s) {
   const size_t Rp = g_.rows_pad;
-  const int rt = g_.row_tiles, ct = g_.col_tiles, r = rank_, W = world_;
+  const int rt = g_.row_tiles, r = rank_, W = world_;
   const size_t blk_t = (size_t)g_.dim_n * g_.ld_t * cs_;
   const size_t slab = Rp * g_.dim_n;  // elements of one contribution slab
   {
@@ -231,17 +231,20 @@ void Engine::backward_sym(const float* grad_out, void* dh, hipStream_t s) {
   NTXENT_HIP_CHECK(hipEventRecord(ev_cdone_, comm_stream_));
   {
     // own contributions while the partners' travel: C_{r,r} Z_r + the full blocks (consecutive
-    // rank blocks r .. r+nfull, two GEMMs if they wrap) + the split block's rows
+    // rank blocks r .. r+nfull, two GEMMs if they wrap) + the split block's rows. The compact
+    // cbuf holds column block r + d at column slots [d * rt, (d + 1) * rt) (sym_c_ld).
     NTXENT_TRACE("ntxent.dz_own");
     // (a local workspace view: the member stays untouched whatever these launches throw)
     GemmWorkspace ws_ovl = ws_;
     ws_ovl.sched_cus = std::max(1, ws_.num_cus - std::min(cfg_.comm_reserve_cus, ws_.num_cus / 2));
-    const int nb = 1 + nfull_, first = std::min(nb, W - r);
-    dz_view(cbuf_, (long)r * rt, ct, zqt_all_, r, 0, first * rt, 0, rt, slabs_, false, false, s, ws_ovl);
-    if (nb > first) dz_view(cbuf_, 0, ct, zqt_all_, 0, 0, (nb - first) * rt, 0, rt, slabs_, true, false, s, ws_ovl);
+    const int nb = 1 + nfull_, first = std::min(nb, W - r), cld = sym_c_ld(g_);
+    dz_view(cbuf_, 0, cld, zqt_all_, r, 0, first * rt, 0, rt, slabs_, false, false, s, ws_ovl);
+    if (nb > first)
+      dz_view(cbuf_, (long)first * rt, cld, zqt_all_, 0, 0, (nb - first) * rt, 0, rt, slabs_, true, false, s, ws_ovl);
     if ((int)jobs_.size() > nfull_) {
       const SymJob& sp = jobs_.back();
-      dz_view(cbuf_, (long)sp.q * rt + sp.k0, ct, zqt_all_, sp.q, (long)sp.k0 * kTile, sp.k1 - sp.k0, sp.m0, sp.m1, slabs_,
+      const int d = ((sp.q - r) % W + W) % W;
+      dz_view(cbuf_, (long)d * rt + sp.k0, cld, zqt_all_, sp.q, (long)sp.k0 * kTile, sp.k1 - sp.k0, sp.m0, sp.m1, slabs_,
               true, false, s, ws_ovl);
     }
   }

@@ -479,8 +479,8 @@ void coef_sym(const at::Tensor& sbuf, const at::Tensor& tiles, const at::Tensor&
   const int4* tp = tile_ptr(tiles, n);
   const auto st = to_scalar(P.bwd());
   NTXENT_CHECK(sbuf.numel() == (long)n * kTileElems && sbuf.scalar_type() == st, "sbuf must hold one tile per entry");
-  NTXENT_CHECK(cbuf.numel() == (long)P.g.row_tiles * P.g.col_tiles * kTileElems && cbuf.scalar_type() == st,
-               "cbuf must be [row_tiles * col_tiles] tiles");
+  NTXENT_CHECK(cbuf.numel() == (long)P.g.row_tiles * sym_c_ld(P.g) * kTileElems && cbuf.scalar_type() == st,
+               "cbuf must be [row_tiles * sym_c_ld] tiles (compact symmetric layout)");
   // partner slots (q - rank - 1) mod W of the cross tiles run 0 .. W/2 - 1 (parallel/symmetric.py)
   NTXENT_CHECK(mbuf.numel() == (long)std::max(1, P.g.world / 2) * P.g.row_tiles * P.g.row_tiles * kTileElems &&
                    mbuf.scalar_type() == st, "mbuf must be [max(1, world/2) * row_tiles * row_tiles] tiles");
@@ -1029,6 +1029,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("compute_dtype", &Plan::compute_dtype)
       .def_property_readonly("backward_dtype", &Plan::backward_dtype_name)
       .def_property_readonly("ld_k8", [](const Plan& p) { return p.g.ld_k8; })
+      .def_property_readonly("sym_c_ld", [](const Plan& p) { return sym_c_ld(p.g); })
       .def_readonly("n_fwd_tiles", &Plan::n_fwd)
       .def_readonly("n_own_tiles", &Plan::n_own)
       .def_readonly("n_dz_tiles", &Plan::n_dz)
@@ -1079,6 +1080,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
+  m.def("fwd_diag_remainder", &ntxent::fwd_diag_remainder, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
+        py::arg("diag_tail"), py::arg("f8") = false);
   m.def("norm_bwd", &norm_bwd, py::arg("slabs"), py::arg("h"), py::arg("inv"), py::arg("grad_out"), py::arg("plan"));
   m.def("fwd_stats_tiles", &fwd_stats_tiles, py::arg("zq_local"), py::arg("zq_chunk"), py::arg("b_tile0"),
         py::arg("tiles"), py::arg("plan"), py::arg("part"), py::arg("reserve_cus") = 0);

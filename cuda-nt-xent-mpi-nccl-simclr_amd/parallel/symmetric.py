@@ -260,11 +260,13 @@ def _split_jobs(jobs: List[Job], rt: int):
 
 
 def sym_coef(C, plan, W, tiles, sc, lse2_all, cpos):
-    """Kept cosines -> (cbuf: this rank's coefficient tiles [row_tiles][col_tiles],
+    """Kept cosines -> (cbuf: this rank's coefficient tiles, compact [row_tiles][plan.sym_c_ld]:
+    column block r + d at column slots [d * rt, (d + 1) * rt) for d = 0 .. W/2, the only blocks a
+    rank writes (5 of 8 at W = 8: 640 instead of 1024 MiB at B = 4096, d = 2048);
     mbuf: the partners' mirrored blocks [slots][row_tiles][row_tiles], slot = job order)."""
     rt = plan.row_tiles
     nslot = max(1, W // 2)  # partner slots (q - r - 1) mod W = 0 .. W/2 - 1
-    cbuf = torch.empty((rt * plan.col_tiles * 65536,), dtype=sc.dtype, device=sc.device)
+    cbuf = torch.empty((rt * plan.sym_c_ld * 65536,), dtype=sc.dtype, device=sc.device)
     mbuf = torch.empty((nslot * rt * rt * 65536,), dtype=sc.dtype, device=sc.device)
     C.coef_sym(sc, tiles, lse2_all, cpos, plan, cbuf, mbuf)
     return cbuf, mbuf
@@ -332,17 +334,19 @@ def sym_norm_bwd(C, plan, own, recv, h, inv, grad_out):
 def sym_own_grad(C, plan, W, r, cbuf, zqt_all, out, reserve_cus=0):
     """This rank's own contributions into ``out`` [Rpad, dim_n]: C_{r,r} Z_r + the full blocks
     C_{r,q} Z_q (one GEMM over the consecutive rank blocks r..r+nfull, two if they wrap) + the
-    split block's rows. The GEMMs leave ``reserve_cus`` CUs free for transfers in flight."""
-    rt, ct = plan.row_tiles, plan.col_tiles
+    split block's rows. The GEMMs leave ``reserve_cus`` CUs free for transfers in flight.
+    ``cbuf`` is the compact layout of :func:`sym_coef` (block r + d at column slots d * rt...)."""
+    rt, cld = plan.row_tiles, plan.sym_c_ld
     full, split = _split_jobs(sym_jobs(W, r, rt), rt)
     nb = 1 + len(full)  # blocks r, r+1, ..., r+nfull (mod W)
     first = min(nb, W - r)
-    C.dz_view(cbuf, r * rt, ct, zqt_all, r, 0, first * rt, 0, rt, out, False, plan, reserve_cus=reserve_cus)
+    C.dz_view(cbuf, 0, cld, zqt_all, r, 0, first * rt, 0, rt, out, False, plan, reserve_cus=reserve_cus)
     if nb > first:
-        C.dz_view(cbuf, 0, ct, zqt_all, 0, 0, (nb - first) * rt, 0, rt, out, True, plan, reserve_cus=reserve_cus)
+        C.dz_view(cbuf, first * rt, cld, zqt_all, 0, 0, (nb - first) * rt, 0, rt, out, True, plan,
+                  reserve_cus=reserve_cus)
     if split is not None:
         q, m0, m1, k0, k1 = split
-        C.dz_view(cbuf, q * rt + k0, ct, zqt_all, q, k0 * 256, k1 - k0, m0, m1, out, True, plan,
+        C.dz_view(cbuf, ((q - r) % W) * rt + k0, cld, zqt_all, q, k0 * 256, k1 - k0, m0, m1, out, True, plan,
                   reserve_cus=reserve_cus)
 
 

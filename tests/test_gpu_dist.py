@@ -73,12 +73,18 @@ def _large_path():
         mod.set_small_path(True)
 
 
-def _close_grad(g, g2, rel=1e-2):
+def _close_grad(h, T, g, g2, rel):
     """The data-parallel stage ops finish the normalisation backward in launch_norm_bwd (dot from
     the fp16 dZ slab); the single-GPU large path fuses it into the dZ epilogue (dot from the
-    coefficient pass): equal up to the rounding of the two dot products (a bf16 output ulp is
-    ~4e-3 of max|g|)."""
-    assert (g.float() - g2.float()).abs().max().item() <= rel * g2.float().abs().max().item()
+    coefficient pass). They differ by design in the last bits, so each is pinned to the fp64
+    oracle at ``rel`` of max|g| (the output dtype's rounding: fp32 inputs 5e-3, bf16 1e-2),
+    rather than to each other at a looser bound."""
+    x = h.detach().double().requires_grad_(True)
+    (gref,) = torch.autograd.grad(R.ntxent_loss(x, T), x)
+    scale = gref.abs().max().item()
+    for name, gg in (("data-parallel", g), ("single-GPU", g2)):
+        err = (gg.double() - gref).abs().max().item()
+        assert err <= rel * scale, (name, err / scale)
 
 
 def test_emulated_world1_equals_single_gpu():
@@ -94,7 +100,7 @@ def test_emulated_world1_equals_single_gpu():
         l2 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
         (g2,) = torch.autograd.grad(l2, x)
     assert loss.item() == l2.item()
-    _close_grad(g, g2)
+    _close_grad(h, 0.07, g, g2, 5e-3)
     # ... and within rounding of the single-launch small-problem path this shape selects
     x = h.clone().requires_grad_(True)
     l3 = ntxent_amd.ntxent_loss(x, 0.07, compute="fp16")
@@ -139,7 +145,7 @@ def test_rccl_path_world1(nccl_world1, overlap):
         l2 = ntxent_amd.ntxent_loss(y, 0.07)
         (g2,) = torch.autograd.grad(l2, y)
     assert loss.item() == l2.item()
-    _close_grad(g, g2)
+    _close_grad(h, 0.07, g, g2, 1e-2)
 
 
 def test_rccl_reduce_scatter_backward_world1(nccl_world1):

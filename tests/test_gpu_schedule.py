@@ -148,6 +148,26 @@ def test_diagonal_remainder_matches_fp64(ext, rows, dim, compute, T):
     _check(h, T, compute, tol)
 
 
+def test_large_diagonal_remainder_runs_diag_up(ext):
+    """A remainder of 48 diagonal tiles (2N = 24576: 4656 own tiles = 18 rounds + 48 on 256 CUs)
+    runs as diag_up regions: round 4 sized the ticket region for at most 36 remainder tiles and
+    sent larger ones to the stream-K third round; the counter region now holds 14
+    tickets per CU."""
+    rows, dim = 24576, 256  # >= 4 K-steps per tile (the remainder path's minimum)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rt = rows // 256
+    n_own = rt * (rt + 1) // 2
+    nk = dim * 2 // 128
+    rem = n_own % cus
+    assert ext.fwd_diag_remainder(n_own, nk, cus, rt) == rem
+    if cus == 256:
+        assert rem == 48
+    plan = ext.get_plan(rows, dim, 1, 0, 0.07, "fp16", 0)
+    assert plan.n_fwd_tiles == n_own and not plan.small
+    h = _views(rows, dim, 53)
+    _check(h, 0.07, "fp16")
+
+
 @pytest.mark.parametrize("rows,dim,compute", [
     (2048, 8192, "fp16"),   # config 4: split-K forward (fp16 slabs) + split-K dZ
     (1024, 4096, "bf16"),

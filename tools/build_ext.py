@@ -144,6 +144,29 @@ def build(force: bool = False, cpp_targets: bool = True, verbose: bool = False) 
     return so
 
 
+def cpp_test_sources():
+    """Every source the C++ test executable is built from (its own file, the kernels, headers and
+    the native runtime; not the torch binding)."""
+    srcs = [ROOT / "tests" / "cpp" / "ntxent_tests.cpp", *KERNEL_SRCS, *_headers()]
+    srcs += [CSRC / "runtime" / n for n in RUNTIME_SRCS]
+    return sorted(srcs, key=lambda p: str(p.relative_to(ROOT)))
+
+
+def source_hash(paths) -> str:
+    """sha256 over (relative path, content) of ``paths``: what a binary was built from, independent
+    of file mtimes (a fresh checkout resets them)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(str(p.relative_to(ROOT)).encode() + b"\0")
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+TESTS_HASH = BUILD / "bin" / "ntxent_tests.srchash"
+
+
 def build_cpp_targets(objs, force: bool = False, verbose: bool = False):
     """Standalone C++ executables (no libtorch): benchmark + tests over the raw API."""
     hdrs = _headers()
@@ -162,6 +185,9 @@ def build_cpp_targets(objs, force: bool = False, verbose: bool = False):
 
     with cf.ThreadPoolExecutor(max_workers=2) as ex:
         list(ex.map(lambda kv: one(*kv), [(n, s) for n, s in targets.items() if s.exists()]))
+    # the sources the (now up-to-date) test binary was built from: tests/test_gpu_cpp_suite.py
+    # refuses a binary whose recorded hash differs from the tree's
+    TESTS_HASH.write_text(source_hash(cpp_test_sources()) + "\n")
 
 
 SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-Xarch_host",

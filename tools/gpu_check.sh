@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 GPU check of the current tree: C++ tests, the whole pytest -m gpu suite (no -x: every
+# GPU check of the current tree: C++ tests, the whole pytest -m gpu suite (no -x: every
 # failure is listed), bench.py x2, rocprofv3 kernel stats of bench.py, native bench at the
-# BASELINE configs. usage: tools/gpu_r4.sh TAG [skip-tests]
+# BASELINE configs. usage: tools/gpu_check.sh TAG [skip-tests]
 set -o pipefail
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r4}; mkdir -p $OUT
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-check}; mkdir -p $OUT
 timeout -k 10 400 build/bin/ntxent_tests > $OUT/cpp_tests.log 2>&1 || { echo "cpp tests failed"; tail -30 $OUT/cpp_tests.log; exit 1; }
 tail -1 $OUT/cpp_tests.log
 if [ "$2" != "skip-tests" ]; then
