@@ -104,3 +104,19 @@ def test_rank_env_maps_rank_r_to_cuda_r(n):
     src = (ROOT / "bench.py").read_text()
     assert 'dist.init_process_group("nccl", device_id=dev' in src
     assert "dev_index = rank_device(local_rank, a.share_gpu)" in src
+
+
+def test_w8_full_check_plumbing_on_cpu(tmp_path):
+    """tools/w8_full_check.py (the config-3-size rehearsal the GPU box runs at W = 8, B = 4096/rank,
+    d = 2048) on CPU tensors over gloo: symmetric vs all-gather vs the fp32 torch oracle, and the
+    one-line JSON it writes."""
+    out = tmp_path / "w.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", "29781",
+                        str(ROOT / "tools" / "w8_full_check.py"), "--device", "cpu", "--batch", "300", "--dim", "48",
+                        "--json-out", str(out)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["ok"] and d["world"] == 3 and len(d["per_rank"]) == 3
+    assert abs(d["loss_symmetric"] - d["loss_fp32_torch"]) <= 1e-5 * abs(d["loss_fp32_torch"])
