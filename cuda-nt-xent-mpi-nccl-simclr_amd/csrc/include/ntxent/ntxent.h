@@ -285,14 +285,18 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 // out_f16: write dZ as fp16 (the reduced-precision plans: half the bytes of the dZ store and of
 // the normalisation backward's read; |dZ| <= ~4, fp16 keeps 11 bits against the bf16/fp16 dh).
 // Fused normalisation backward of the dZ GEMM's epilogue: dh = grad_out/(2N tau) inv (g - z dot)
-// computed per tile from the fp16-staged g, h, inv and dot (launch_dot_reduce); the dZ slab is
-// not written. The launchers return whether they fused (not for fp32 plans or d % 8 != 0: then
-// the slab is written and launch_norm_bwd runs).
+// computed per tile from the fp16-staged g, h, inv and dot; the dZ slab is not written. The
+// launchers return whether they fused (not for fp32 plans or d % 8 != 0: then the slab is
+// written and launch_norm_bwd runs).
+// dot: either dotp (the coefficient pass's slot partials, dot_slots(g) x Rpad: the dZ epilogue
+// sums its tile's rows itself, or launch_dz runs launch_dot_reduce into `dot` for the split-K
+// reduce path, so `dot` must then be a writable Rpad buffer), or a reduced dot (dotp null).
 struct NormFuse {
   const void* h = nullptr;
   DType in = DType::BF16;
   const float* inv = nullptr;
   const float* dot = nullptr;
+  const float* dotp = nullptr;
   const float* grad_out = nullptr;  // device scalar
   void* dh = nullptr;
 };

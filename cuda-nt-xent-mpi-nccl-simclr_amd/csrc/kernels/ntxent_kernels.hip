@@ -811,7 +811,10 @@ int apply_schedule(dev::SimParams& p, int ntiles, const GemmWorkspace& ws, hipSt
 
 // Leading dimension (elements) for a row of `n` elements: strides of a multiple of 1024
 // elements get 64 extra so the rows a tile streams rotate through the L2 channels.
-int padded_ld(int n) { return (n % 1024 == 0) ? n + 64 : n; }
+#ifndef NTXENT_NO_LDPAD
+#define NTXENT_NO_LDPAD 0  // A/B switch (tools/build_variant.sh -DNTXENT_NO_LDPAD=1: unpadded rows)
+#endif
+int padded_ld(int n) { return (!NTXENT_NO_LDPAD && n % 1024 == 0) ? n + 64 : n; }
 
 // The coefficient tiles as the dZ GEMM's A operand: tile (I, J) of a row panel of `panel_tiles`
 // tiles; 256 K-columns per tile. Row-major tiles: rows of 256 elements, every 256 K-columns jump
@@ -1357,6 +1360,8 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
   p.nd = g.dim;
   p.ninv = nf->inv;
   p.ndot = nf->dot;
+  p.ndotp = nf->dotp;
+  p.nslot = dot_slots(g);
   p.ngo = nf->grad_out;
   p.nalpha = (float)(1.0 / ((double)g.global_rows * g.temperature));
   p.ndh = nf->dh;
@@ -1422,7 +1427,14 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     grid = apply_schedule(p, ntiles, ws, stream);
   }
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
-  if (fused) NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot");
+  if (fused) NTXENT_CHECK(nf->dot != nullptr || (nf->dotp != nullptr && pieces == 0),
+                          "dz: fused normalisation backward without dot");
+  if (fused && p.ndotp && pieces > 0) {
+    // the split-K reduce finishes rows per fragment: reduce the slots once for it
+    launch_dot_reduce(nf->dotp, const_cast<float*>(nf->dot), g, stream);
+    p.ndotp = nullptr;
+  }
+  if (fused && p.ndotp) NTXENT_CHECK(p.nslot % 2 == 0, "dz: odd dot slot count");
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);
