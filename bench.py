@@ -23,7 +23,6 @@ fewer GPUs than asked).
 from __future__ import annotations
 
 import argparse
-import gc
 import json
 import math
 import os
@@ -89,8 +88,6 @@ def parse(argv=None):
                          "at steps 10-19, 0.44 from step 60 on: profiles/r2/ramp); reported in the JSON")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="launcher: seconds before the whole job is killed; ranks: process-group timeout")
-    ap.add_argument("--gc-pause", default="on", choices=["on", "off"],
-                    help="pause Python's cyclic GC inside the timed bracket (as timeit does; off: leave it running)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args(argv)
 
@@ -297,15 +294,10 @@ def run_rank(a) -> None:
     def timed(step, steps, warmup, per_step_events=True, comm=False):
         """warmup untimed steps, then exactly `steps` steps bracketed by barrier + synchronize
         on both sides; returns (total s, per-step ms list or None, comm ms per step or None).
-        Python's cyclic garbage collector is paused inside the bracket (as ``timeit`` does): a
-        collection pause while the GPU queue is shallow, right after the synchronize, idles the
-        GPU for a whole step (BENCH_r04's event pass: one 0.72 ms step among 0.40 ms ones)."""
+        (Python's cyclic GC stays on: paused inside the bracket, the steps' autograd garbage piled up
+        and the allocator's growth made them 0.46-0.47 ms instead of 0.406, profiles/r5/bench_gc.)"""
         for _ in range(warmup):
             loss, gh = step()
-        gc_was = gc.isenabled() and a.gc_pause == "on"
-        if gc_was:
-            gc.collect()
-            gc.disable()
         sync()
         barrier()
         sync()
@@ -324,8 +316,6 @@ def run_rank(a) -> None:
         barrier()
         sync()
         dt = time.perf_counter() - t0
-        if gc_was:
-            gc.enable()
         timed.host_ms = (t_enq - t0) / steps * 1e3
         per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)] if evs else None
         comm_ms = None
@@ -463,7 +453,6 @@ def run_rank(a) -> None:
             "step_ms_source": ("HIP events around each of %d steps, a separate pass after the timed region "
                                "(one untimed step first)" % min(a.steps, 20)) if per_ms else None,
             "host_enqueue_ms_per_step": round(host_ms, 4),
-            "gc_paused_in_timed_region": a.gc_pause == "on",
             "host_enqueue_note": ("host CPU time to issue one step (autograd graph + kernel launches) in the "
                                   "timed run, max over ranks; the GPU is the bottleneck while it is below "
                                   "ms_per_step"),

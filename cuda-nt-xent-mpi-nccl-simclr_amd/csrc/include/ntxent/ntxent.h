@@ -235,8 +235,9 @@ int lse_scratch_floats(const Geometry& g);
 // fp8 backward (FP8 plans, set_fp8_backward; world 1, kept cosines): the coefficient matrix and
 // Z^T go to the dZ GEMM as e4m3. C row i is scaled by 2^q8_row_exp(mneg2_i, lmin) (a bound on
 // its negatives from the LSE pass; the positive C_ip is excluded and added exactly in the dZ
-// epilogue), Z^T by 256. Q8Stats carries the LSE pass's extra outputs: mneg2 [Rpad] (each row's
-// negatives-only max logit, log2 units), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
+// epilogue), Z^T by 256. Q8Stats carries the LSE pass's extra outputs: mneg2 [Rpad] (a bound on
+// each row's largest negative logit, log2 units: max over the column tiles of m + log2 s, within
+// log2(256) of it), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
 // bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
 void set_fp8_backward(bool on);  // default off (opt-in: 5e-2 of max|g| gradient error)
 bool fp8_backward_enabled();
@@ -288,15 +289,14 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 // computed per tile from the fp16-staged g, h, inv and dot; the dZ slab is not written. The
 // launchers return whether they fused (not for fp32 plans or d % 8 != 0: then the slab is
 // written and launch_norm_bwd runs).
-// dot: either dotp (the coefficient pass's slot partials, dot_slots(g) x Rpad: the dZ epilogue
-// sums its tile's rows itself, or launch_dz runs launch_dot_reduce into `dot` for the split-K
-// reduce path, so `dot` must then be a writable Rpad buffer), or a reduced dot (dotp null).
+// dot: the reduced z_i . g_i (launch_dot_reduce). (Summing the coefficient pass's slots in the dZ
+// epilogue instead measured slower: dZ +4.6 / +6.3 / +10 us at the headline / config 4 / config 5
+// against the 5-6 us launch it removes, profiles/r5/variants_dotfold.)
 struct NormFuse {
   const void* h = nullptr;
   DType in = DType::BF16;
   const float* inv = nullptr;
   const float* dot = nullptr;
-  const float* dotp = nullptr;
   const float* grad_out = nullptr;  // device scalar
   void* dh = nullptr;
 };

@@ -207,7 +207,9 @@ __global__ __launch_bounds__(256) void prep_kernel(const Tin* __restrict__ h, Tc
 // Wave-per-pair prologue for d % 8 == 0, d <= 512 * NCH: each lane keeps its NCH chunks of 8
 // features of both rows in registers between the norm and the normalise pass (h is read once)
 // and every reduction is a wave reduction (no LDS, no block barrier); 4 pairs per block.
-template <typename Tin, typename Tc, bool Q8, int NCH>
+// ST (statistics only, the raw-operand forward): inv and ypos from the input rows in fp32, no zq
+// (ypos = (h_i . h_p) inv_i inv_p, unrounded; no pad blocks).
+template <typename Tin, typename Tc, bool Q8, int NCH, bool ST = false>
 __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
                                                         float* __restrict__ inv, float* __restrict__ ypos,
                                                         int R, int d, int dk, int ldk, float y_scale,
@@ -247,6 +249,19 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
   ssp = wave_sum(ssp);
   const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
   const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  if constexpr (ST) {
+    float hd = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hd += a[c][j] * b[c][j];
+    hd = wave_sum(hd);
+    if (lane == 0) {
+      inv[i] = ivi; inv[pi] = ivp;
+      ypos[i] = hd * ivi * ivp * y_scale; ypos[pi] = ypos[i];
+    }
+    return;
+  }
   // fp8: per-row power-of-two scale from the row's amax (amax of z = amax of h * inv exactly)
   int ei = 0, ep = 0;
   if constexpr (Q8) {
@@ -295,7 +310,7 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
 // Block-per-pair prologue for 2048 < d <= 2048 * NCH (d % 8 == 0): as prep_wave_kernel with 256
 // threads per pair, each thread keeping its NCH chunks of 8 features of both rows in registers,
 // so h is read once (the generic prep_kernel reads it twice: 1.5x the HBM traffic at d = 8192).
-template <typename Tin, typename Tc, bool Q8, int NCH>
+template <typename Tin, typename Tc, bool Q8, int NCH, bool ST = false>
 __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__ h, Tc* __restrict__ zq,
                                                          float* __restrict__ inv, float* __restrict__ ypos,
                                                          int R, int d, int dk, int ldk, float y_scale,
@@ -333,6 +348,19 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
   ssp = block_sum(ssp, red + 8);
   const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
   const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  if constexpr (ST) {  // statistics only (see prep_wave_kernel)
+    float hd = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hd += a[c][j] * b[c][j];
+    hd = block_sum(hd, red);
+    if (t == 0) {
+      inv[i] = ivi; inv[pi] = ivp;
+      ypos[i] = hd * ivi * ivp * y_scale; ypos[pi] = ypos[i];
+    }
+    return;
+  }
   int ei = 0, ep = 0;
   if constexpr (Q8) {
     ei = fp8_row_exp(block_max(mxi, red) * ivi);
@@ -377,16 +405,31 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
 // gathers (V rows r = V jc + q of one column per lane group) hit distinct banks (the padded
 // linear layout alone left them 4-way conflicted: 3.7M SQ_LDS_BANK_CONFLICT per launch at the
 // headline, profiles/r2/pmc_final).
-template <typename T>
-__device__ __forceinline__ void transpose_tile(const T* __restrict__ zq, T* __restrict__ zqt, int dk, int ldk, int ldt,
-                                               int bx, int by, T (&tile)[64][64 + 16 / sizeof(T)]) {
+// Ts / inv (raw-operand forward): the source rows are the input h (2-byte Ts, same width as T),
+// normalised here (z = h * inv[row]) on their way into the tile.
+template <typename T, typename Ts = T>
+__device__ __forceinline__ void transpose_tile(const Ts* __restrict__ zq, T* __restrict__ zqt, int dk, int ldk, int ldt,
+                                               int bx, int by, T (&tile)[64][64 + 16 / sizeof(T)],
+                                               const float* __restrict__ inv = nullptr) {
   constexpr int V = 16 / sizeof(T);  // elements per 16 B
   constexpr int CPR = 64 / V;        // 16-B chunks per 64-element row
+  static_assert(sizeof(Ts) == sizeof(T), "transpose: source and destination element widths differ");
   const int j0 = bx * 64, e0 = by * 64;
   for (int k = threadIdx.x; k < 64 * CPR; k += 256) {
     const int r = k / CPR, c = k % CPR;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (e0 + c * V < dk) v = *reinterpret_cast<const u32x4*>(zq + (long long)(j0 + r) * ldk + e0 + c * V);
+    if constexpr (!std::is_same<Ts, T>::value || sizeof(T) == 2) {
+      if (inv) {  // (uniform) raw rows: normalise, convert
+        const float s = inv[j0 + r];
+        union { Ts h[V]; u32x4 u; } x;
+        union { T h[V]; u32x4 u; } y;
+        x.u = v;
+#pragma unroll
+        for (int q = 0; q < V; ++q) y.h[q] = from_f32<T>(to_f32<Ts>(x.h[q]) * s);
+        v = y.u;
+      }
+    }
     *reinterpret_cast<u32x4*>(&tile[r][(c ^ ((r / V) % CPR)) * V]) = v;
   }
   __syncthreads();
@@ -491,6 +534,12 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
   if (item < n) {  // uniform across the 8 lanes of an item
     const int i = item, j = item + n;
     float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
+    // fp8 backward: a bound on each row's largest negative logit, max over the column tiles of
+    // m + log2(s) (>= the tile's largest term, <= it + log2(256)). The merged m alone is no bound:
+    // the fixed-shift forward epilogue reports m = M (the largest POSSIBLE logit) for every tile,
+    // and a scale from it put the negatives' coefficients ~15 bits below their e4m3 range
+    // (subnormal or zero: a 5e-2 gradient error, profiles/r5/fp8bwd_diag.log).
+    float bi = kNegInf, bj = kNegInf;
     // 4 column tiles per lane per round, all loads issued before the (branchy) merges: one
     // memory round trip per 32 column tiles instead of one per tile
     for (int t0 = q; t0 < Tc; t0 += 4 * kLseLanes) {
@@ -507,12 +556,20 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
         if (t0 + u * kLseLanes < Tc) {
           lse_merge(mi, si, vi[u].x, vi[u].y);
           lse_merge(mj, sj, vj[u].x, vj[u].y);
+          if (a.mneg2) {
+            bi = fmaxf(bi, vi[u].y > 0.f ? vi[u].x + log2f(vi[u].y) : kNegInf);
+            bj = fmaxf(bj, vj[u].y > 0.f ? vj[u].x + log2f(vj[u].y) : kNegInf);
+          }
         }
     }
 #pragma unroll
     for (int off = 1; off < kLseLanes; off <<= 1) {
       lse_merge(mi, si, __shfl_xor(mi, off), __shfl_xor(si, off));
       lse_merge(mj, sj, __shfl_xor(mj, off), __shfl_xor(sj, off));
+      if (a.mneg2) {
+        bi = fmaxf(bi, __shfl_xor(bi, off));
+        bj = fmaxf(bj, __shfl_xor(bj, off));
+      }
     }
     if (q == 0) {
       const float yp = a.ypos[i];
@@ -524,7 +581,7 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
       cpos[j] = -(a_i + a_j);
       li = l_i + l_j;
       lmn = fminf(L2i, L2j);
-      if (a.mneg2) { a.mneg2[own0 + i] = mi; a.mneg2[own0 + j] = mj; }
+      if (a.mneg2) { a.mneg2[own0 + i] = bi; a.mneg2[own0 + j] = bj; }
     }
   } else if (item < Rpad - n && q == 0) {
     const int i = R + (item - n);
@@ -579,9 +636,10 @@ __global__ __launch_bounds__(256) void lse_kernel(const LseArgs a) {
 // blocks and the transpose is bandwidth-bound on many, so they share the chip instead of
 // running back to back, and no side stream / event join (a ~5-7 us bubble each) is needed.
 // Q8: the transpose writes the fp8 backward's e4m3(256 Z^T) (T = _Float16 rows in).
-template <typename T, bool Q8 = false>
-__global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int nb, const T* __restrict__ zq,
-                                                            void* __restrict__ zqt, int dk, int ldk, int ldt, int tx) {
+template <typename T, bool Q8 = false, typename Ts = T>
+__global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int nb, const Ts* __restrict__ zq,
+                                                            void* __restrict__ zqt, int dk, int ldk, int ldt, int tx,
+                                                            const float* __restrict__ inv = nullptr) {
   __shared__ __attribute__((aligned(16))) T tile[64][64 + 16 / sizeof(T)];
   __shared__ float red[16];
   __shared__ int last;
@@ -592,7 +650,7 @@ __global__ __launch_bounds__(256) void lse_transpose_kernel(const LseArgs a, int
     if constexpr (Q8)
       transpose_tile_q8(zq, static_cast<unsigned char*>(zqt), dk, ldk, ldt, t % tx, t / tx, tile);
     else
-      transpose_tile<T>(zq, static_cast<T*>(zqt), dk, ldk, ldt, t % tx, t / tx, tile);
+      transpose_tile<T, Ts>(zq, static_cast<T*>(zqt), dk, ldk, ldt, t % tx, t / tx, tile, inv);
   }
 }
 
@@ -1040,6 +1098,34 @@ void launch_prep(DType in, DType comp, const void* h, void* zq, float* inv, floa
   const float ys = g.inv_temp * dev::kLog2e;
   // wave-per-pair kernel when the rows fit in registers (d <= 2048), else one block per pair
   const int nch = (g.dim % 8 == 0) ? (g.dim + 511) / 512 : 0;
+  if (zq == nullptr) {  // statistics only (raw-operand forward): inv, ypos; no zq, no pad rows
+    NTXENT_CHECK(zq8 == nullptr && g.dim % 8 == 0 && g.dim <= 16384, "prep (statistics only): d % 8 == 0, d <= 16384");
+    dispatch_comp(in, [&](auto tin) {
+      using Tin = decltype(tin);
+      if (nch >= 1 && nch <= 4) {
+        auto go = [&](auto nc) {
+          hipLaunchKernelGGL((dev::prep_wave_kernel<Tin, Tin, false, decltype(nc)::value, true>),
+                             dim3((g.rows / 2 + 3) / 4), dim3(256), 0, stream, static_cast<const Tin*>(h), nullptr, inv,
+                             ypos, g.rows, g.dim, g.dim_k, g.ld_k, ys, nullptr, 0, 0, g.rows);
+        };
+        if (nch == 1) go(std::integral_constant<int, 1>{});
+        else if (nch == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 4>{});
+      } else {
+        const int nbl = (g.dim + 2047) / 2048;
+        auto go = [&](auto nc) {
+          hipLaunchKernelGGL((dev::prep_block_kernel<Tin, Tin, false, decltype(nc)::value, true>), dim3(g.rows / 2),
+                             dim3(256), 0, stream, static_cast<const Tin*>(h), nullptr, inv, ypos, g.rows, g.dim,
+                             g.dim_k, g.ld_k, ys, nullptr, 0, 0);
+        };
+        if (nbl <= 2) go(std::integral_constant<int, 2>{});
+        else if (nbl <= 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 8>{});
+      }
+    });
+    NTXENT_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dispatch_comp(in, [&](auto tin) {
     using Tin = decltype(tin);
     dispatch_comp(comp, [&](auto tc) {
@@ -1360,8 +1446,6 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
   p.nd = g.dim;
   p.ninv = nf->inv;
   p.ndot = nf->dot;
-  p.ndotp = nf->dotp;
-  p.nslot = dot_slots(g);
   p.ngo = nf->grad_out;
   p.nalpha = (float)(1.0 / ((double)g.global_rows * g.temperature));
   p.ndh = nf->dh;
@@ -1427,14 +1511,7 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     grid = apply_schedule(p, ntiles, ws, stream);
   }
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
-  if (fused) NTXENT_CHECK(nf->dot != nullptr || (nf->dotp != nullptr && pieces == 0),
-                          "dz: fused normalisation backward without dot");
-  if (fused && p.ndotp && pieces > 0) {
-    // the split-K reduce finishes rows per fragment: reduce the slots once for it
-    launch_dot_reduce(nf->dotp, const_cast<float*>(nf->dot), g, stream);
-    p.ndotp = nullptr;
-  }
-  if (fused && p.ndotp) NTXENT_CHECK(p.nslot % 2 == 0, "dz: odd dot slot count");
+  if (fused) NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot");
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);

@@ -104,9 +104,7 @@ struct SimParams {
   const void* nh;        // dZ epilogue: input rows h [R][nd] (dtype nh_dt: 0 fp32, 1 fp16, 2 bf16) ...
   int nh_dt, nd;
   const float* ninv;     // ... 1 / |h_i|
-  const float* ndot;     // ... dot_i (reduced dotp), or
-  const float* ndotp;    // ... the coefficient pass's slot partials [nslot][Rpad], summed by dz_store
-  int nslot;
+  const float* ndot;     // ... dot_i (reduced dotp)
   const float* ngo;      // ... grad_out (device scalar)
   float nalpha;          // ... 1 / (2N tau)
   void* ndh;             // ... output dh [R][nd] (non-null: fused epilogue)
@@ -697,10 +695,9 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
     // and its 16 chunks of h (16-bit inputs) right after it, so their latency hides under the
     // staging and the barriers instead of following the tile's last MFMA one load at a time
     float iv0 = 0.f, dt0 = 0.f;
-    const int drow = mt * kTile + (tid & (kTile - 1));
-    if (p.ndh && tid < kTile && drow < p.R) {
-      iv0 = p.ninv[drow];
-      if (!p.ndotp) dt0 = p.ndot[drow];
+    if (p.ndh && tid < kTile && mt * kTile + tid < p.R) {
+      iv0 = p.ninv[mt * kTile + tid];
+      dt0 = p.ndot[mt * kTile + tid];
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -713,27 +710,6 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
         for (int r = 0; r < 4; ++r) pk.h[r] = (_Float16)acc[mi][ni][r];
         *(lds_u2*)(lds + rt * 512 + ((((ct >> 3) ^ (rt & 15))) << 4) + ((ct >> 2) & 1) * 8) = pk.u;
       }
-    }
-    typedef __attribute__((address_space(3))) float lds_fl;
-    if (p.ndh && p.ndotp) {
-      // dot_i = sum over the coefficient pass's slots (the dot_reduce launch folded in): threads t
-      // and t + 256 sum the two halves of row t's slots, 32 loads in flight, in slot order
-      // (deterministic); the halves meet in LDS after the staging barrier
-      const int half = tid >> 8, ns = p.nslot >> 1;
-      float part = 0.f;
-      if (drow < p.R) {
-        const float* src = p.ndotp + (long long)(half * ns) * p.Rpad + drow;
-        int k = 0;
-        for (; k + 32 <= ns; k += 32) {  // (no per-load condition: hipcc would branch and wait per load)
-          float v[32];
-#pragma unroll
-          for (int u = 0; u < 32; ++u) v[u] = src[(long long)(k + u) * p.Rpad];
-#pragma unroll
-          for (int u = 0; u < 32; ++u) part += v[u];
-        }
-        for (; k < ns; ++k) part += src[(long long)k * p.Rpad];
-      }
-      ((lds_fl*)(lds + kTile * 512 + 2048))[tid] = part;
     }
     const bool h16 = p.ndh && p.nh_dt != 0;
     u32x4 hq[16];
@@ -754,12 +730,9 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
       // with dot_m = z_m . g_m = sum_j C_mj cos_mj from the coefficient pass. g is the fp16 tile
       // staged above (the precision of the unfused fp16 dZ slab).
       const float sgo = p.ngo[0] * p.nalpha;
+      typedef __attribute__((address_space(3))) float lds_fl;
       lds_fl* cf = (lds_fl*)(lds + kTile * 512);  // [256][2] per-row c1, c2
       if (tid < kTile) {
-        if (p.ndotp) {
-          const lds_fl* dp2 = (const lds_fl*)(lds + kTile * 512 + 2048);
-          dt0 = dp2[tid] + dp2[kTile + tid];
-        }
         cf[2 * tid] = sgo * iv0;
         cf[2 * tid + 1] = sgo * iv0 * iv0 * dt0;
       }
@@ -852,7 +825,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   constexpr int kScaleLds = MODE == kModeCoef ? kCoefLds : kGemmLds;
   // (+2 KiB: fp8 row scales, or the fused dZ epilogue's per-row coefficients; forward: + 12 KiB
   // of row / column reductions above the stage buffers, see the prologue prefetch)
-  constexpr int kFwdRed = kScaleLds + (MODE == kModeDz ? 4096 : std::is_same<T, fp8e4m3>::value ? 2048 : 0);
+  constexpr int kFwdRed = kScaleLds + ((std::is_same<T, fp8e4m3>::value || MODE == kModeDz) ? 2048 : 0);
   __shared__ __attribute__((aligned(16))) char smem[kFwdRed + (MODE == kModeFwd ? 6 * 256 * 8 : 0)];
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;

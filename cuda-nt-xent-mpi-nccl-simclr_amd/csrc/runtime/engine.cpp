@@ -241,7 +241,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
-    // (the dZ epilogue sums dotp_ itself: NormFuse::dotp)
+    if (fuse_) launch_dot_reduce(dotp_, dot_, g_, s);
   }
   if (zqt_pending_) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));
@@ -255,7 +255,6 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     nf.in = cfg_.input;
     nf.inv = inv_;
     nf.dot = dot_;
-    nf.dotp = dotp_;
     nf.grad_out = grad_out ? grad_out : one_;
     nf.dh = dh;
     const bool fused =

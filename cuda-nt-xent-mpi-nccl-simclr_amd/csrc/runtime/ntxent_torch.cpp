@@ -727,15 +727,13 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   at::Tensor dh, go;
   NormFuse nf;
   if (fuse) {
-    // the dZ epilogue sums the coefficient pass's dot slots itself (launch_dz reduces them into
-    // `dot` only for its split-K path)
+    launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
     go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
     dh = at::empty_like(h);
     nf.h = h.data_ptr();
     nf.in = to_dtype(h.scalar_type());
     nf.inv = inv.data_ptr<float>();
     nf.dot = dot.data_ptr<float>();
-    nf.dotp = dp;
     nf.grad_out = go.data_ptr<float>();
     nf.dh = dh.data_ptr();
   }

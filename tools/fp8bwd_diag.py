@@ -66,6 +66,53 @@ def main():
     # relative error of the row direction (what the optimiser sees)
     rel = ((g8 - g16).norm(dim=1) / g16.norm(dim=1).clamp_min(1e-30))
     print(f"per-row relative L2 error: median {rel.median().item():.3e}, max {rel.max().item():.3e} (row {int(rel.argmax())})")
+    emulate(C, h, a, g8, g16)
+
+
+def emulate(C, h, a, g8, g16):
+    """torch emulation from the same plan's stage ops: the fp16 coefficient tiles of the fp8 forward
+    (coef), reassembled, against e4m3 copies of C (per-row power-of-two scale from the row's
+    actual max) and of 256 z; both through the same normalisation backward. Says what e4m3 operands
+    cost by themselves, next to what the kernels' two backwards differ by."""
+    plan = C.get_plan(a.rows, a.dim, 1, 0, a.T, "fp8", 0)
+    zq, inv, ypos, zq8 = C.prep(h, plan)
+    part, sc = C.fwd_stats(zq8, zq8, plan, True)
+    lse2 = torch.empty((plan.rows_pad,), dtype=torch.float32, device="cuda")
+    cpos = torch.empty_like(lse2)
+    C.lse(part, ypos, lse2, cpos, plan)
+    cb = C.coef(sc, lse2, cpos, plan)
+    torch.cuda.synchronize()
+    rt, ct, R, d = plan.row_tiles, plan.col_tiles, a.rows, a.dim
+    Cf = cb.view(rt, ct, 256, 256).permute(0, 2, 1, 3).reshape(rt * 256, ct * 256)[:R, :R].float()
+    z = zq[:R, :d].float()
+    n = R // 2
+    pos = (torch.arange(R, device="cuda") + n) % R
+    ar = torch.arange(R, device="cuda")
+    cp = Cf[ar, pos].clone()
+    alpha = 1.0 / (R * a.T)
+
+    def dh(dz):
+        dz = dz * alpha
+        return inv[:R, None] * (dz - z * (z * dz).sum(1, keepdim=True))
+
+    d16 = dh(Cf @ z)
+    Cn = Cf.clone()
+    Cn[ar, pos] = 0.0
+    rmax = Cn.abs().amax(1, keepdim=True).clamp_min(1e-30)
+    e = torch.floor(torch.log2(448.0 / rmax))
+    Cq = (Cn * 2.0 ** e).clamp(-448, 448).to(torch.float8_e4m3fn).float() / 2.0 ** e
+    Zq = (256 * z).to(torch.float8_e4m3fn).float() / 256
+    d8 = dh(Cq @ Zq + cp[:, None] * z[pos])
+    s = d16.abs().max().item()
+    print(f"emulated: max|dh(e4m3 C, e4m3 z) - dh(fp16 C)| / max = {(d8 - d16).abs().max().item() / s:.3e}; "
+          f"e4m3 C only {(dh(Cq @ z + cp[:, None] * z[pos]) - d16).abs().max().item() / s:.3e}; "
+          f"e4m3 z only {(dh(Cf @ Zq - cp[:, None] * Zq[pos] + cp[:, None] * z[pos]) - d16).abs().max().item() / s:.3e}")
+    sk = g16.abs().max().item()
+    print(f"kernel fp16 backward vs emulated fp16: {(g16 - d16).abs().max().item() / sk:.3e}; "
+          f"kernel fp8 backward vs emulated fp16: {(g8 - d16).abs().max().item() / sk:.3e}; "
+          f"vs emulated e4m3: {(g8 - d8).abs().max().item() / sk:.3e}")
+    print(f"C: positive |C_ip| median {cp.abs().median().item():.3e}; negatives row max median {rmax.median().item():.3e}; "
+          f"negatives row sum median {Cn.sum(1).median().item():.3e}")
 
 
 if __name__ == "__main__":
