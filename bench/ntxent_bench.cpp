@@ -425,6 +425,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-small") o.small = false;
     else if (a == "--fp8-bwd") ntxent::set_fp8_backward(true);
     else if (a == "--no-fp8-bwd") ntxent::set_fp8_backward(false);
+    else if (a == "--no-raw-fwd") ntxent::set_raw_forward(false);
     else if (a == "--small-splits") o.small_splits = std::stoi(next());
     else if (a == "--negatives") {
       const std::string v = next();
@@ -445,6 +446,7 @@ int main(int argc, char** argv) {
                   "           or N emulated ranks on GPU 0 (in-process ThreadComm, --emulate)\n"
                   "  --gpus N --proc-rank r --uid-file F [--shared-gpu]: rank r of N processes over RCCL\n"
                   "  --fp8-bwd / --no-fp8-bwd: with --compute fp8, the backward's C and Z^T in e4m3 too (or fp16)\n"
+                  "  --no-raw-fwd: unit-row (zq) forward operands instead of the input rows normalised in the epilogue\n"
                   "  --small-fuse-rows R: small forward with the row prologue fused up to R rows (0: prep launch)\n"
                   "  --grad-digest: print a hash of dh after one step (build variants must match bitwise)\n"
                   "  (the measured A/B alternatives of earlier rounds are deleted; build-time variants:\n"

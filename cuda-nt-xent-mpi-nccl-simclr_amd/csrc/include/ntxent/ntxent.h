@@ -200,11 +200,24 @@ struct BlockView {
 // remainder of at most that many tiles after its whole rounds, the remainder runs as upper 64x64
 // regions in a second, short launch (diag_up_kernel) instead of a third round or a stream-K
 // split (528 forward tiles at B = 4096/view: 2 rounds + 16 diagonal tiles instead of ~2.9 rounds).
+// Raw-operand forward (single process, 2-byte input rows, kept cosines): the forward GEMM reads
+// the input rows h themselves (their own dtype: bf16 input -> bf16 MFMA operands, exact; fp16 ->
+// fp16) and normalises in its epilogue (cos = acc inv_i inv_j), the LSE launch transposes h * inv
+// into Z^T, and the row prologue only computes inv and the positive logits (launch_prep with
+// zq = null): no zq rows are written or read (prep 32 MiB lighter at the headline).
+struct RawRows {
+  const void* h = nullptr;      // [rows][dim] input rows
+  DType in = DType::BF16;       // their dtype (F16 or BF16)
+  const float* inv = nullptr;   // [rows] 1 / |h_i|
+};
+bool raw_forward_eligible(const Geometry& g, DType in, DType comp);  // world 1, 2-byte in & comp, rows % 256, dim % 64
+void set_raw_forward(bool on);  // default on (off: the zq path, for A/B and tests)
+bool raw_forward_enabled();
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
                       const BlockView& bv = BlockView{}, float2* part_x = nullptr,
-                      int diag_tail = 0, hipEvent_t main_done = nullptr);
+                      int diag_tail = 0, hipEvent_t main_done = nullptr, const RawRows* raw = nullptr);
 // main_done (optional): recorded on `stream` right after the persistent GEMM, before the remainder.
 // Split-K for own-block launches with fewer tiles than CUs and long K (BASELINE config 4): K
 // pieces of every tile publish partial slabs and a second launch sums them and runs the
@@ -249,10 +262,11 @@ struct Q8Stats {
   void* zq8t = nullptr;
   const void* zq = nullptr;  // fp16 rows (the dZ epilogue's positive term C_ip z_p)
 };
+// raw (raw-operand forward): the transpose reads raw->h and writes Z^T = (h * inv)^T in tr_dtype.
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos,
                 float* block_loss, float* loss_sum, const Geometry& g, hipStream_t stream,
                 DType tr_dtype = DType::F16, const void* zq = nullptr, void* zqt = nullptr,
-                const Q8Stats* q8 = nullptr);
+                const Q8Stats* q8 = nullptr, const RawRows* raw = nullptr);
 
 // Kept cosine tiles `sbuf` ([n_fwd_tiles][256*256], fragment order) -> coefficient tiles
 // `cbuf` ([row_tiles][col_tiles][256*256], row-major per tile) with C = P + P^T - 2 I_pos;

@@ -86,6 +86,11 @@ template <> struct Mfma<fp8e4m3> {
 // (fp8 GEMMs keep their outputs in fp16: the backward runs in fp16).
 template <typename T> struct StoreT { typedef T type; };
 template <> struct StoreT<fp8e4m3> { typedef _Float16 type; };
+// Raw-operand forward on bf16 input rows (the input h itself, normalised in the epilogue): bf16
+// MFMA operands, cosines kept in fp16 for the fp16 backward.
+struct bf16r {};
+template <> struct Mfma<bf16r> : Mfma<__bf16> {};
+template <> struct StoreT<bf16r> { typedef _Float16 type; };
 
 // E8M0 byte -> 2^(byte - 127) as fp32 (bytes 1..254: normal powers of two).
 __device__ __forceinline__ float e8m0_to_f32(unsigned char b) { return __int_as_float((int)b << 23); }
@@ -144,6 +149,18 @@ __device__ __forceinline__ float wave_sum(float x) {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void lds_put_f2(unsigned addr, f32x2 v) {
   asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+// untracked 4- and 16-byte LDS reads (usable while LDS-DMA is in flight: a compiler-tracked
+// LDS access there makes hipcc wait vmcnt(0))
+__device__ __forceinline__ float lds_get_f32(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ f32x4 lds_get_f32x4(unsigned addr) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+  return v;
 }
 // four 8-byte reads at addr + {0, 1, 2, 3} * 2048
 __device__ __forceinline__ void lds_get4_f2(unsigned addr, f32x2& a, f32x2& b, f32x2& c, f32x2& d) {

@@ -1204,6 +1204,7 @@ static std::atomic<bool> g_small_path{true};     // one-launch small-problem for
 static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
 static std::atomic<int> g_small_fuse_rows{-1};   // small forward: fused row prologue up to R rows (-1: default)
 static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
+static std::atomic<bool> g_raw_fwd{true};        // raw-operand forward (RawRows) where eligible
 void set_small_path(bool on) { g_small_path = on; }
 bool small_path_enabled() { return g_small_path.load(); }
 void set_small_splits(int n) { g_small_splits = std::max(0, n); }
@@ -1211,6 +1212,13 @@ int small_splits_override() { return g_small_splits.load(); }
 void set_small_fuse_rows(int rows) { g_small_fuse_rows = rows < 0 ? -1 : rows; }
 int small_fuse_rows_override() { return g_small_fuse_rows.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
+void set_raw_forward(bool on) { g_raw_fwd = on; }
+bool raw_forward_enabled() { return g_raw_fwd.load(); }
+bool raw_forward_eligible(const Geometry& g, DType in, DType comp) {
+  // (fp16 rows on a bf16 plan would keep fp16 cosines for a bf16 backward: not offered)
+  return g.world == 1 && (in == DType::F16 || in == DType::BF16) && (comp == DType::F16 || comp == in) &&
+         g.rows % kTile == 0 && g.dim % 64 == 0 && g.dim <= 16384;
+}
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
 int q8_ldt(const Geometry& g) { return g.rows_pad; }
@@ -1241,13 +1249,23 @@ int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
 void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
                       hipStream_t stream, const BlockView& bv, float2* part_x, int diag_tail,
-                      hipEvent_t main_done) {
+                      hipEvent_t main_done, const RawRows* raw) {
   if (ntiles == 0) return;
   NTXENT_CHECK(diag_tail >= 0 && diag_tail <= ntiles, "fwd_stats: bad diagonal tail");
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
+  if (raw) {
+    NTXENT_CHECK(raw_forward_eligible(g, raw->in, comp) && raw->inv && part_x == nullptr && bv.b_tile0 == 0,
+                 "fwd_stats (raw operands): single-process 2-byte plan, rows % 256 == 0, dim % 64 == 0");
+    zq_local = zq_all = raw->h;
+  }
+  // raw operands: the input rows, dim (= dim_k) elements apart; else the padded zq rows
   const long long kb = f8 ? (long long)g.dim_k8 : (long long)g.dim_k * dtype_size(comp);
-  const long long ld = f8 ? (long long)g.ld_k8 : (long long)g.ld_k * dtype_size(comp);
+  const long long ld = f8 ? (long long)g.ld_k8 : raw ? (long long)g.dim * 2 : (long long)g.ld_k * dtype_size(comp);
   dev::SimParams p = base_params(g);
+  if (raw) {
+    p.inv_a = raw->inv;
+    p.inv_b = raw->inv;
+  }
   set_operand_scales(p, comp, g);
   p.A = rowmajor_operand(zq_local, ld, kb);
   p.B = rowmajor_operand(zq_all, ld, kb);
@@ -1296,7 +1314,13 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   } else {
     grid = apply_schedule(p, nmain, ws, stream);
   }
-  dispatch_gemm(comp, [&](auto tc) {
+  // operand type: the plan's, or for raw bf16 rows on an fp16 plan bf16 operands with fp16 kept
+  // cosines (dev::bf16r)
+  auto dispatch_fwd = [&](auto&& f) {
+    if (raw && raw->in == DType::BF16 && comp == DType::F16) f(dev::bf16r{});
+    else dispatch_gemm(comp, f);
+  };
+  dispatch_fwd([&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeFwd>(grid, p, stream);
     if (pieces > 0) {
@@ -1370,7 +1394,7 @@ int lse_scratch_floats(const Geometry& g) { return 64 + 2 * lse_blocks(g); }  //
 
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
                 float* loss_sum, const Geometry& g, hipStream_t stream, DType tr_dtype, const void* zq, void* zqt,
-                const Q8Stats* q8) {
+                const Q8Stats* q8, const RawRows* raw) {
   const int nb = lse_blocks(g);  // one workgroup per 32 pairs / pad rows
   dev::LseArgs a{part, ypos, lse2_all, cpos, block_loss, loss_sum, (float)(1.0 / (double)g.global_rows),
                  g.rows, g.rows_pad, g.col_tiles, g.rank * g.rows_pad};
@@ -1378,7 +1402,23 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
     a.mneg2 = q8->mneg2;
     a.lmin = q8->lmin;
   }
-  if (zq == nullptr) {
+  if (raw) {  // Z^T = (h * inv)^T straight from the input rows (raw-operand forward)
+    NTXENT_CHECK(zqt != nullptr && q8 == nullptr && raw->inv && (tr_dtype == DType::F16 || tr_dtype == DType::BF16) &&
+                     g.rows == g.rows_pad && g.dim == g.dim_k, "lse (raw rows): 2-byte Z^T, rows % 256 == 0, dim % 64 == 0");
+    const int tx = g.rows_pad / 64, ty = g.dim_n / 64;
+    dispatch_comp(tr_dtype, [&](auto tc) {
+      using Tc = decltype(tc);
+      auto go = [&](auto ts) {
+        using Ts = decltype(ts);
+        hipLaunchKernelGGL((dev::lse_transpose_kernel<Tc, false, Ts>), dim3(nb + tx * ty), dim3(256), 0, stream, a, nb,
+                           static_cast<const Ts*>(raw->h), zqt, g.dim, g.dim, g.ld_t, tx, raw->inv);
+      };
+      if constexpr (sizeof(Tc) == 2) {
+        if (raw->in == DType::BF16) go(__bf16{});
+        else go(_Float16{});
+      }
+    });
+  } else if (zq == nullptr) {
     hipLaunchKernelGGL(dev::lse_kernel, dim3(nb), dim3(256), 0, stream, a);
   } else if (q8 && q8->zq8t) {
     NTXENT_CHECK(tr_dtype == DType::F16 && g.world == 1, "lse: the fp8 backward transposes fp16 rows (world 1)");

@@ -83,6 +83,10 @@ struct SimParams {
   int b_tile0;           // B operand: global column tile of the chunk's first row tile (ring mode)
   int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
   int c_rot;             // symmetric mode: column slot (nt - row_tile0) mod col_tiles instead (sym_c_ld)
+  // raw-operand forward (RawRows): A / B are the input rows h, not unit rows; the accumulators are
+  // normalised by inv_a[A row] * inv_b[B row] before the epilogue (null: unit-row operands)
+  const float* inv_a;
+  const float* inv_b;
   float y_scale;         // inv_temp * log2(e) = M, the largest possible logit (log2 units)
   float acc_scale;       // logit (log2 units) per accumulator unit (y_scale)
   int scale_off;         // fp8 operands: byte offset of each row's E8M0 scale (= K bytes of a row)
@@ -826,7 +830,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // (+2 KiB: fp8 row scales, or the fused dZ epilogue's per-row coefficients; forward: + 12 KiB
   // of row / column reductions above the stage buffers, see the prologue prefetch)
   constexpr int kFwdRed = kScaleLds + ((std::is_same<T, fp8e4m3>::value || MODE == kModeDz) ? 2048 : 0);
-  __shared__ __attribute__((aligned(16))) char smem[kFwdRed + (MODE == kModeFwd ? 6 * 256 * 8 : 0)];
+  // forward: + 12 KiB of row / column reductions, + 4 KiB: the raw-operand ring of row inverse
+  // norms (2 slots x [256 A rows | 256 B rows], filled by 4-byte LDS-DMA one item ahead)
+  constexpr int kInvLds = kFwdRed + (MODE == kModeFwd ? 6 * 256 * 8 : 0);
+  __shared__ __attribute__((aligned(16))) char smem[kInvLds + (MODE == kModeFwd && !std::is_same<T, fp8e4m3>::value ? 4096 : 0)];
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
@@ -869,6 +876,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   f32x4 acc[8][4];
   constexpr bool kF8 = std::is_same<T, fp8e4m3>::value;
+  // raw-operand forward: thread t stages inv of A row t (t < 256) or B row t - 256 of tile (mt, nt)
+  // into ring slot `slot` (one 4-byte LDS-DMA per lane, wave-linear destination)
+  auto stage_inv = [&](int mt_, int nt_, int slot) {
+    if constexpr (MODE == kModeFwd && !kF8) {
+      const int t = threadIdx.x;
+      const float* src = t < kTile ? p.inv_a + (long long)mt_ * kTile + t : p.inv_b + (long long)(nt_ - p.b_tile0) * kTile + (t - kTile);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kInvLds + slot * 2048 + 256 * w), 4, 0, 0);
+    }
+  };
   // fp8: the MFMA runs with unit E8M0 scales (127); the rows' power-of-two scales are applied to
   // the accumulators before the epilogue (exact). Per-lane scale operands loaded per tile cost a
   // vmcnt(0) drain of the prologue DMA (a plain load's first use with LDS-DMA in flight).
@@ -1037,8 +1053,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   };
   // operand streams of an item + its prologue DMA: A0 B0 B1 A1 of step 0, A0 B0 B1 of step 1
   // (the stream clamps keep the trailing prefetches in bounds, so every wait count is uniform)
-  auto prologue = [&](int tile, int kb, int ke) {
+  auto prologue = [&](int tile, int kb, int ke, int slot) {
     const int4 tt = sload_int4(p.tiles, tile);
+    if (p.inv_a) stage_inv(tt.x, tt.y, slot);
     const int ns = ke - kb;
     const char* Ab = p.A.base + (long long)tt.x * p.A.row_tile_stride;
     const char* Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
@@ -1067,15 +1084,18 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     tile = bid + item * G; kb = 0; ke = nk; stile = -1;
   } else {
     if (!fetch(item, tile, kb, ke, stile)) break;
-    prologue(tile, kb, ke);
+    prologue(tile, kb, ke, item & 1);
   }
   const bool cont = streaming && item + 1 < n_dp;  // the trailing stages stage the next item
   const char* na = nullptr;
   const char* nb = nullptr;
+  int nmt = 0, nnt = 0;
   if (cont) {
     const int4 tn = sload_int4(p.tiles, bid + (item + 1) * G);
     na = p.A.base + (long long)tn.x * p.A.row_tile_stride;
     nb = p.B.base + (long long)(tn.y - p.b_tile0) * p.B.row_tile_stride;
+    nmt = tn.x;
+    nnt = tn.y;
   }
   const int4 t = sload_int4(p.tiles, tile);
   const int mt = t.x, nt = t.y;
@@ -1097,6 +1117,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
       if (cont && ks == nsteps - 2) {
         sa0.init(na, 0, p.A, nk); sb0.init(nb, 0, p.B, nk); sb1.init(nb, 0, p.B, nk);
+        // the next item's row inverse norms, into the other ring slot (older than every stage
+        // still to come: the counted waits before its epilogue retire it)
+        if (p.inv_a) stage_inv(nmt, nnt, (item + 1) & 1);
       }
       if (cont && ks == nsteps - 1) sa1.init(na, 0, p.A, nk);
     }
@@ -1179,6 +1202,26 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) cb[ni] = 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1);
 
+  if constexpr (MODE == kModeFwd && !kF8) {
+    if (p.inv_a) {
+      // raw operands: cos = acc * inv_a[row] * inv_b[col], before any split-K publication (linear)
+      // and the epilogue; the ring slot was filled one item ahead (or by this item's prologue)
+      // and retired by the main loop's counted waits and barriers (untracked reads: the next
+      // item's DMA may be in flight)
+      const unsigned ib = (unsigned)(uintptr_t)(lds + kInvLds) + (unsigned)((item & 1) * 2048);
+      float cs[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) cs[ni] = lds_get_f32(ib + 4 * (kTile + cb[ni] + (lane & 15)));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        const f32x4 rs = lds_get_f32x4(ib + 4 * (rb[mi] + 4 * (lane >> 4)));
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= rs[r] * cs[ni];
+      }
+    }
+  }
   if (nsteps != nk && !sk_fixup<kF8>(acc, p, stile, bid, G, tid, smem)) continue;
 
   if constexpr (MODE == kModeDz) {
@@ -1556,6 +1599,15 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
     buf = buf == NSt - 1 ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
+  if (p.inv_a) {  // raw operands: normalise (lane: rows 64a + 16w + 4 (lane >> 4) + r, cols 64b + 16f + (lane & 15))
+    const f32x4 rs = *reinterpret_cast<const f32x4*>(p.inv_a + (long long)mt * kTile + 64 * a + 16 * w + 4 * (lane >> 4));
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float cs = p.inv_b[(long long)(nt - p.b_tile0) * kTile + 64 * b + 16 * f + (lane & 15)];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[f][r] *= rs[r] * cs;
+    }
+  }
   int* flag = reinterpret_cast<int*>(smem + kSubStages * kSubStage + 4 * 64 * 8);
   int* cnt_pair = p.sk_cnt + 4 * nt_d;  // [nt_d][10] after the [nt_d][4] row-group tickets
   if (nkp > 1) {

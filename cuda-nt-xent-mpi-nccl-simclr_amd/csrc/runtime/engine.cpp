@@ -144,7 +144,13 @@ void Engine::forward(const void* h, hipStream_t s) {
   const size_t Rp = g_.rows_pad;
   char* zq_local = zq_all_ + (size_t)rank_ * Rp * g_.ld_k * cs_;
   char* zqt_local = zqt_all_ + (size_t)rank_ * g_.dim_n * g_.ld_t * cs_;
-  // forward GEMM operand: the e4m3 rows for fp8 plans, else zq itself
+  const bool raw = world_ == 1 && !small_ && !f8_ && cfg_.keep_cos && raw_forward_enabled() &&
+                   raw_forward_eligible(g_, cfg_.input, cfg_.compute);
+  RawRows rr;
+  rr.h = h;
+  rr.in = cfg_.input;
+  rr.inv = inv_;
+  // forward GEMM operand: the e4m3 rows for fp8 plans, else zq itself (or the input rows: raw)
   char* op_all = f8_ ? zq8_all_ : zq_all_;
   const size_t op_bytes = f8_ ? Rp * g_.ld_k8 : Rp * g_.ld_k * cs_;
   char* op_local = op_all + (size_t)rank_ * op_bytes;
@@ -161,7 +167,8 @@ void Engine::forward(const void* h, hipStream_t s) {
       if (fault_armed("nonfinite")) NTXENT_HIP_CHECK(hipMemsetAsync(loss_, 0xFF, 4, s));  // NaN
       return;
     }
-    launch_prep(cfg_.input, bwd_, h, zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
+    // raw-operand forward (RawRows): no unit rows at all, the prologue computes inv and ypos only
+    launch_prep(cfg_.input, bwd_, h, raw ? nullptr : zq_local, inv_, ypos_, g_, s, f8_ ? op_local : nullptr);
     // world 1: the transpose is written by the LSE launch (beside the merge, see below)
     if (world_ > 1) launch_transpose(bwd_, zq_local, zqt_local, g_, s);
   }
@@ -183,7 +190,7 @@ void Engine::forward(const void* h, hipStream_t s) {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s, BlockView{},
-                     nullptr, own_diag_tail(g_));
+                     nullptr, own_diag_tail(g_), nullptr, raw ? &rr : nullptr);
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");
@@ -201,7 +208,8 @@ void Engine::forward(const void* h, hipStream_t s) {
       q8.zq8t = zq8t_;
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
     } else if (world_ == 1)
-      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, zqt_local);
+      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, raw ? nullptr : zq_local, zqt_local,
+                 nullptr, raw ? &rr : nullptr);
     else
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
   }

@@ -617,6 +617,35 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
                      small_scratch(h, *P).data_ptr(), P->g, cur_stream(h));
     return {loss, zq, at::Tensor(), inv, lse2, at::Tensor(), arow};
   }
+  const DType in = to_dtype(h.scalar_type());
+  if (keep_cos && comp != DType::FP8 && raw_forward_enabled() && raw_forward_eligible(P->g, in, comp)) {
+    // raw-operand forward (RawRows): the GEMM reads h itself and normalises in its epilogue; the
+    // prologue only computes inv and the positive logits, the LSE launch writes Z^T = (h inv)^T.
+    // zq is returned empty (0 elements, the backward dtype): nothing reads unit rows
+    auto inv = at::empty({P->g.rows}, opts(h, at::kFloat));
+    auto ypos = at::empty({P->g.rows}, opts(h, at::kFloat));
+    auto s = cur_stream(h);
+    launch_prep(in, P->bwd(), h.data_ptr(), nullptr, inv.data_ptr<float>(), ypos.data_ptr<float>(), P->g, s);
+    RawRows raw;
+    raw.h = h.data_ptr();
+    raw.in = in;
+    raw.inv = inv.data_ptr<float>();
+    auto part = at::empty({P->g.col_tiles, P->g.rows_pad, 2}, opts(h, at::kFloat));
+    auto sc = at::empty({(long)P->n_fwd * kTileElems}, opts(h, to_scalar(P->bwd())));
+    auto ws = gemm_ws(h, P->n_fwd, *P);
+    launch_fwd_stats(P->comp, nullptr, nullptr, reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd,
+                     reinterpret_cast<float2*>(part.data_ptr<float>()), sc.data_ptr(), ws, P->g, s, BlockView{}, nullptr,
+                     P->n_fwd == P->n_own ? own_diag_tail(P->g) : 0, nullptr, &raw);
+    auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+    auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
+    auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, opts(h, to_scalar(P->bwd())));
+    auto block_loss = device_scratch(h, (size_t)lse_scratch_floats(P->g) * 4, 1);
+    auto loss = at::empty({}, opts(h, at::kFloat));
+    launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(), lse2.data_ptr<float>(),
+               cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()), loss.data_ptr<float>(), P->g, s,
+               P->bwd(), nullptr, zqt.data_ptr(), nullptr, &raw);
+    return {loss, at::empty({0}, opts(h, to_scalar(P->bwd()))), zqt, inv, lse2, sc, cpos};
+  }
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
   // ZqT (the dZ GEMM's B operand) is first read in the backward: the LSE launch writes it from
   // extra blocks beside the merge (one stream: a side-stream transpose cost an event record and
@@ -722,7 +751,9 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   if (sc_in.has_value() && sc_in->defined()) {
     cb = coef(*sc_in, lse2, cpos, *P, dp);
   } else {
-    cb = coef_gemm(zq, zq, lse2, cpos, *P, dp);
+    // (a raw-operand forward returns no unit rows: a second backward rebuilds them to recompute S)
+    const at::Tensor zr = zq.numel() > 0 ? zq : prep(h, *P, c10::nullopt, c10::nullopt)[0];
+    cb = coef_gemm(zr, zr, lse2, cpos, *P, dp);
   }
   at::Tensor dh, go;
   NormFuse nf;
@@ -1077,6 +1108,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                         const Plan& P) { return coef_gemm(zl, za, lse2_all, cpos, P); });
   m.def("dz", [](const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P) { return dz(sc, zqt_all, P); });
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
+  m.def("set_raw_forward", &ntxent::set_raw_forward, py::arg("on"));
+  m.def("raw_forward_enabled", &ntxent::raw_forward_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
