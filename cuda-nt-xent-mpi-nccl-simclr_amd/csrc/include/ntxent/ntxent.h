@@ -252,10 +252,10 @@ int lse_scratch_floats(const Geometry& g);
 // each row's largest negative logit, log2 units: max over the column tiles of m + log2 s, within
 // log2(256) of it), lmin [1] (the smallest LSE), and zq8t [dim_n][q8_ldt]
 // bytes = e4m3(256 zq^T) written instead of zqt (zq: fp16 rows).
-void set_fp8_backward(bool on);  // default off (opt-in: 5e-2 of max|g| gradient error)
+void set_fp8_backward(bool on);  // default on (gradient within bf16 rounding of the fp16 backward's)
 bool fp8_backward_enabled();
 bool fp8_backward_eligible(const Geometry& g, DType comp);  // FP8 plan, world 1, dim % 8 == 0
-int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes) = Rpad
+int q8_ldt(const Geometry& g);                               // row stride of zq8t (bytes): Rpad, padded
 struct Q8Stats {
   float* mneg2 = nullptr;
   float* lmin = nullptr;

@@ -1198,12 +1198,12 @@ void launch_transpose(DType comp, const void* zq, void* zqt, const Geometry& g, 
 // ---- runtime switches: every process-wide toggle of the library lives here (atomics). Only
 //      behaviour switches remain: the small-problem path (off = the large-problem pipeline at
 //      every shape, so tests can exercise it on small inputs), its two test overrides, and the
-//      opt-in fp8 backward. Measured A/B losers are deleted, not kept behind toggles; the CUs a
+//      fp8 backward switch. Measured A/B losers are deleted, not kept behind toggles; the CUs a
 //      GEMM leaves free for communication are a per-launch argument (GemmWorkspace::sched_cus).
 static std::atomic<bool> g_small_path{true};     // one-launch small-problem forward / backward
 static std::atomic<int> g_small_splits{0};       // small backward column splits (0: small_bwd_splits)
 static std::atomic<int> g_small_fuse_rows{-1};   // small forward: fused row prologue up to R rows (-1: default)
-static std::atomic<bool> g_fp8_bwd{false};       // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
+static std::atomic<bool> g_fp8_bwd{true};        // FP8 plans: e4m3 coefficient / Z^T dZ GEMM (Q8Stats)
 static std::atomic<bool> g_raw_fwd{true};        // raw-operand forward (RawRows) where eligible
 void set_small_path(bool on) { g_small_path = on; }
 bool small_path_enabled() { return g_small_path.load(); }
@@ -1221,7 +1221,10 @@ bool raw_forward_eligible(const Geometry& g, DType in, DType comp) {
 }
 bool fp8_backward_enabled() { return g_fp8_bwd.load(); }
 bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType::FP8 && g.world == 1 && g.dim % 8 == 0; }
-int q8_ldt(const Geometry& g) { return g.rows_pad; }
+// padded like the 16-bit Z^T (padded_ld): at a power-of-two stride (16 KiB at config 5) the dZ's
+// B half-tiles, 8 rows per DMA instruction, all fell into one L1 set and L2 channel (TD busy 86 %,
+// MFMA busy 17 %: profiles/r5/fp8_dz)
+int q8_ldt(const Geometry& g) { return (!NTXENT_NO_LDPAD && g.rows_pad % 1024 == 0) ? g.rows_pad + 128 : g.rows_pad; }
 
 // K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel): 2 from 32 K-steps
 // up (the headline: 1 piece +2 us), 1 below (config 2 -1.5 us, config 5 -0.4 us:

@@ -387,16 +387,21 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
 // stored tile and 2^e_j for its mirror (row j of the lower tile); the positive entry is stored as
 // 0 (the dZ epilogue adds C_ip z_p exactly). Both byte tiles are staged in LDS (stride 80 B: the
 // column-major writes hit distinct banks) and leave as 16-byte row segments. A lane's 4 rows of
-// one column pack into a dword (the mirror's layout); for the stored tile a quad of lanes swaps
-// bytes by DPP so that each lane holds 4 consecutive columns of one row.
-__device__ __forceinline__ unsigned q8_pack4(const float (&x)[4], float sc) {
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(x[0] * sc, -448.f), 448.f),
-                                          fminf(fmaxf(x[1] * sc, -448.f), 448.f), 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(x[2] * sc, -448.f), 448.f), fminf(fmaxf(x[3] * sc, -448.f), 448.f),
-                                      w, true);
-  return (unsigned)w;
+// one column pack into a dword (the mirror's layout); for the stored tile a quad of lanes
+// transposes its 4 x 4 bytes in two DPP + v_perm stages, so that each lane holds 4 consecutive
+// columns of one row. The dot partials use the dequantised C (as the dZ GEMM reads it) with the
+// power-of-two scale factored out of the sums. The pass is VALU-bound (at 2.6 TB/s in round 4),
+// so the plain regions (no self, positive or padding element: uniform per wave) skip the masks.
+__device__ __forceinline__ unsigned q8_pack4(float x0, float x1, float x2, float x3) {  // x >= 0
+  const int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(x0, 448.f), fminf(x1, 448.f), 0, false);
+  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(fminf(x2, 448.f), fminf(x3, 448.f), w, true);
 }
-__device__ __forceinline__ float q8_byte(unsigned w, int b) { return __builtin_amdgcn_cvt_f32_fp8((int)(w >> (8 * b)), 0); }
+// sum_r e4m3(w byte r) * a[r]
+__device__ __forceinline__ float q8_dot4(unsigned w, const f32x4& a) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false), hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+  return fmaf(lo[0], a[0], fmaf(lo[1], a[1], fmaf(hi[0], a[2], hi[1] * a[3])));
+}
 
 template <typename TS>
 __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (&rb)[4], const int (&cb)[4],
@@ -407,14 +412,13 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   lds_char* ld_m = lds + 64 * S8;   // mirror: [64 cols][64 rows]
   unsigned char* base = reinterpret_cast<unsigned char*>(p.cbuf);
   unsigned char* slot = base + ctile_index(p, mt, nt) * kTileElems;
-  unsigned char* mirror = (kind == kTileSymOff || kind == kTileDiagUp)
-                              ? base + ctile_index(p, nt - p.row_tile0, p.row_tile0 + mt) * kTileElems
-                              : nullptr;
+  const bool mirrored = kind == kTileSymOff || kind == kTileDiagUp;
+  unsigned char* mirror = mirrored ? base + ctile_index(p, nt - p.row_tile0, p.row_tile0 + mt) * kTileElems : nullptr;
   const int col_local0 = (nt * kTile) % p.Rpad;
   const bool fixed = p.fixed_shift != 0;
   const float M = p.y_scale;
   const float lmin = p.q8_lmin[0];
-  float lcol[4], scol[4], icol[4];
+  float lcol[4], scol[4];
   bool cvalid[4];
   int gj[4];
 #pragma unroll
@@ -424,67 +428,70 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
     const float l = p.lse2[gj[ni]];
     lcol[ni] = fixed ? fast_exp2(M - l) : l;
     cvalid[ni] = (col_local0 + col_t) < p.R;
-    const int e = q8_row_exp(p.q8_mneg[gj[ni]], lmin);
-    scol[ni] = exp2i(e);
-    icol[ni] = exp2i(-e);
+    scol[ni] = exp2i(q8_row_exp(p.q8_mneg[gj[ni]], lmin));
   }
+  // plain region: as coef_epilogue
+  const int r_lo = mt * kTile + row_base, r_hi = r_lo + 64;
+  const int c_lo = nt * kTile + col_base, c_hi = c_lo + 64;
+  auto hits = [&](int a0) { return a0 < c_hi && c_lo < a0 + 64; };
+  const bool plain = fixed && r_hi <= p.R && col_local0 + col_base + 64 <= p.R && !hits(p.own0 + r_lo) &&
+                     !hits(p.own0 + r_lo + p.n_half) && !hits(p.own0 + r_lo - p.n_half);
   const int wq = col_base >> 6;
-  float cdot[4] = {0.f, 0.f, 0.f, 0.f};
-  const int qd = lane & 3;  // the row of a 4-row group this lane stores after the quad swap
+  float cdot[4] = {0.f, 0.f, 0.f, 0.f}, cposd[4] = {0.f, 0.f, 0.f, 0.f};
+  // quad byte transpose (lane q of a quad holds bytes M[q][0..3]; afterwards T[q][r] = M[r][q]):
+  // exchange 16-bit halves with lane q ^ 2, then bytes with lane q ^ 1
+  const int qd = lane & 3;
+  const unsigned sel1 = qd < 2 ? 0x05040100u : 0x03020706u;
+  const unsigned sel2 = (qd & 1) ? 0x03070105u : 0x06020400u;
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
     const int row_t0 = rb[mi] + 4 * (lane >> 4);
     const int gi0 = mt * kTile + row_t0;
     const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
-    const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
     const f32x4 mneg4 = *reinterpret_cast<const f32x4*>(p.q8_mneg + p.own0 + gi0);
-    float srow[4], irow[4], rdot[4] = {0.f, 0.f, 0.f, 0.f};
+    float srow[4], lrow[4], rdot[4] = {0.f, 0.f, 0.f, 0.f}, rposd[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int e = q8_row_exp(mneg4[r], lmin);
-      srow[r] = exp2i(e);
-      irow[r] = exp2i(-e);
+      srow[r] = exp2i(q8_row_exp(mneg4[r], lmin));
+      lrow[r] = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
     }
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       float c[4];
-      bool pos[4];
+      if (plain) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = gi0 + r;
-        const bool rvalid = gi < p.R;
-        const float lrow = fixed ? fast_exp2(M - lrow4[r]) : lrow4[r];
-        const int gself = p.own0 + gi;
-        const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
-        const float y = acc[mi][ni][r] * p.acc_scale;
-        float v = fixed ? fast_exp2(y - M) * (lrow + lcol[ni]) : fast_exp2(y - lrow) + fast_exp2(y - lcol[ni]);
-        const bool ok = rvalid && cvalid[ni] && gj[ni] != gself;
-        pos[r] = ok && gj[ni] == gpos;
-        c[r] = (ok && !pos[r]) ? v : 0.0f;
-      }
-      // stored tile: byte r of w_d = row r at this lane's column, each with its row's scale
-      unsigned w_d = 0;
+        for (int r = 0; r < 4; ++r) c[r] = fast_exp2(acc[mi][ni][r] * p.acc_scale - M) * (lrow[r] + lcol[ni]);
+      } else {
+        const f32x4 cpos4 = *reinterpret_cast<const f32x4*>(p.cpos + gi0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int b = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(c[r] * srow[r], 448.f), 0.f, 0, false) & 0xff;
-        w_d |= (unsigned)b << (8 * r);
-        const float dq = pos[r] ? cpos4[r] : q8_byte((unsigned)b, 0) * irow[r];
-        rdot[r] += dq * acc[mi][ni][r];
+        for (int r = 0; r < 4; ++r) {
+          const int gi = gi0 + r;
+          const int gself = p.own0 + gi;
+          const int gpos = p.own0 + (gi < p.n_half ? gi + p.n_half : gi - p.n_half);
+          const float y = acc[mi][ni][r] * p.acc_scale;
+          const float v = fixed ? fast_exp2(y - M) * (lrow[r] + lcol[ni]) : fast_exp2(y - lrow[r]) + fast_exp2(y - lcol[ni]);
+          const bool ok = gi < p.R && cvalid[ni] && gj[ni] != gself;
+          const bool pos = ok && gj[ni] == gpos;
+          c[r] = (ok && !pos) ? v : 0.0f;
+          // the positive entry is exact in the dZ epilogue; its dot term likewise
+          const float pd = pos ? cpos4[r] * acc[mi][ni][r] : 0.f;
+          rposd[r] += pd;
+          cposd[ni] += pd;
+        }
       }
-      // mirror: 4 rows of column j, scaled by column j's row scale
-      const unsigned w_m = q8_pack4(c, scol[ni]);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float dq = pos[r] ? cpos4[r] : q8_byte(w_m, r) * icol[ni];
-        cdot[ni] += dq * acc[mi][ni][r];
+      const unsigned w_d = q8_pack4(c[0] * srow[0], c[1] * srow[1], c[2] * srow[2], c[3] * srow[3]);
+      const unsigned w_m = q8_pack4(c[0] * scol[ni], c[1] * scol[ni], c[2] * scol[ni], c[3] * scol[ni]);
+      if (p.dotp) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w_d, false), hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w_d, true);
+        rdot[0] = fmaf(lo[0], acc[mi][ni][0], rdot[0]);
+        rdot[1] = fmaf(lo[1], acc[mi][ni][1], rdot[1]);
+        rdot[2] = fmaf(hi[0], acc[mi][ni][2], rdot[2]);
+        rdot[3] = fmaf(hi[1], acc[mi][ni][3], rdot[3]);
+        if (mirrored) cdot[ni] += q8_dot4(w_m, acc[mi][ni]);
       }
-      // quad byte swap: lane 4k + qd gathers row qd of columns 4k .. 4k+3 of this 16-column group
-      const unsigned s0 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0x00, 0xf, 0xf, false);  // quad_perm [k,k,k,k]
-      const unsigned s1 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0x55, 0xf, 0xf, false);
-      const unsigned s2 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0xaa, 0xf, 0xf, false);
-      const unsigned s3 = (unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0xff, 0xf, 0xf, false);
-      const unsigned o = ((s0 >> (8 * qd)) & 0xffu) | (((s1 >> (8 * qd)) & 0xffu) << 8) |
-                         (((s2 >> (8 * qd)) & 0xffu) << 16) | (((s3 >> (8 * qd)) & 0xffu) << 24);
+      const unsigned t1 = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)w_d, 0x4e, 0xf, 0xf, false), w_d, sel1);
+      const unsigned o = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)t1, 0xb1, 0xf, 0xf, false), t1, sel2);
       const int cl = cb[ni] - col_base + (lane & 12);  // first of the 4 columns (region-local)
       *(__attribute__((address_space(3))) unsigned*)(ld_d + (row_t0 - row_base + qd) * S8 + cl) = o;
       *(__attribute__((address_space(3))) unsigned*)(ld_m + (cb[ni] - col_base + (lane & 15)) * S8 +
@@ -493,15 +500,15 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
     if (p.dotp) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float d = row16_sum(rdot[r]);
+        const float d = row16_sum(fmaf(rdot[r], exp2i(-q8_row_exp(mneg4[r], lmin)), rposd[r]));
         if ((lane & 15) == 0) p.dotp[(long long)(nt * 4 + wq) * p.Rpad + gi0 + r] = d;
       }
     }
   }
-  if (p.dotp && (kind == kTileSymOff || kind == kTileDiagUp)) {
+  if (p.dotp && mirrored) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      const float d = xrow_sum(cdot[ni]);
+      const float d = xrow_sum(fmaf(cdot[ni], exp2i(-q8_row_exp(p.q8_mneg[gj[ni]], lmin)), cposd[ni]));
       const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
       if (lane < 16) p.dotp[(long long)((p.row_tile0 + mt) * 4 + (row_base >> 6)) * p.Rpad + row] = d;
     }
@@ -847,17 +854,19 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const int nk = p.nk;                       // K-steps of a whole tile
   KStream sa0, sa1, sb0, sb1;
 
-  // per-lane source offsets of this wave's two 8-row pieces of each half-tile
-  unsigned a_off[2][2], b_off[2][2];
+  // source offsets of this wave's two 8-row pieces j of each half-tile h: row 128 h + 16 w + 8 j +
+  // (lane >> 3); the per-lane part (row in the piece, swizzled 16-B chunk: bits 1-3 of the row
+  // come from 8 j + (lane >> 3) alone) in 2 VGPRs per operand, the wave-uniform part as the DMA's
+  // scalar offset (8 VGPRs of per-(h, j) offsets made the fp8 dZ spill them inside the main loop:
+  // 18 VGPRs: the fp8 dZ 641 -> 196 us at config 5 with the read bases below, profiles/r5/fp8_dz)
+  unsigned a_vo[2], b_vo[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = 128 * h + 16 * w + 8 * j + (lane >> 3);
-      const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
-      a_off[h][j] = (unsigned)(row * p.A.ld) + lchunk * 16;
-      b_off[h][j] = (unsigned)(row * p.B.ld) + lchunk * 16;
-    }
+  for (int j = 0; j < 2; ++j) {
+    const int rl = 8 * j + (lane >> 3);
+    const int lchunk = (lane & 7) ^ ((rl >> 1) & 7);
+    a_vo[j] = (unsigned)((lane >> 3) * p.A.ld) + lchunk * 16;
+    b_vo[j] = (unsigned)((lane >> 3) * p.B.ld) + lchunk * 16;
+  }
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     // LDS layout [A even | A odd | B even | B odd] (32 KiB each): every operand read of either
@@ -869,8 +878,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(s.ptr), 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8 * j * kKStepBytes), 16,
-                                               isB ? b_off[h][j] : a_off[h][j], 0, 0, kGemmDmaAux);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8 * j * kKStepBytes), 16, isB ? b_vo[j] : a_vo[j],
+                                               (unsigned)((128 * h + 16 * w + 8 * j) * (isB ? p.B.ld : p.A.ld)), 0,
+                                               kGemmDmaAux);
     s.advance(isB ? p.B : p.A);
   };
 
@@ -897,16 +907,27 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   constexpr int NS = kF8 ? 1 : 2;
   typedef __attribute__((address_space(3))) const i32x4 lds_i4;
   OP af[NS][4], bf0[NS][2], bf1[NS][2];
+  // operand-read lane bases, one per k-substep s and operand (row 64 wa + r16 of A / 32 wb + r16 of
+  // B, swizzled chunk 4 s + cq): every read is one of them + a compile-time immediate (buffer,
+  // half-tile, row block). Opaque: formed inside the reads, the fp8 kernels' substep-1 addresses
+  // were (row base + block offset) + chunk, three more loop-invariant VGPRs that the dZ spilled
+  // and reloaded behind a vmcnt(0) in every K-step (profiles/r5/fp8_dz).
+  unsigned rd_a[2], rd_b[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const unsigned pch = (unsigned)(((4 * s + cq) ^ sw) << 4);
+    rd_a[s] = (unsigned)((64 * wa + r16) * kKStepBytes) + pch;
+    rd_b[s] = (unsigned)(kStageBytes + (32 * wb + r16) * kKStepBytes) + pch;
+    asm volatile("" : "+v"(rd_a[s]), "+v"(rd_b[s]));
+  }
   auto read_a = [&](int buf, int h, OP (&af)[NS][4]) {
-    const lds_char* As = lds + buf * (kTile * kKStepBytes);
     i32x4 lo[4];  // fp8: k-substep 0, joined with substep 1 into a fully (re)defined operand (a
                   // .lo/.hi partial write would keep the other half live across the whole kernel)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int pch = ((4 * s + cq) ^ sw) << 4;
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
-        const lds_char* src = As + (128 * h + 64 * wa + 16 * mi + r16) * kKStepBytes + pch;
+        const lds_char* src = lds + rd_a[s] + (buf * kTile + 128 * h + 16 * mi) * kKStepBytes;
         if constexpr (kF8) {
           if (s == 0) lo[mi] = *(lds_i4*)src;
           else af[0][mi] = __builtin_shufflevector(lo[mi], *(lds_i4*)src, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -917,14 +938,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   };
   auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
-    const lds_char* Bs = lds + kStageBytes + buf * (kTile * kKStepBytes);
     i32x4 lo[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int pch = ((4 * s + cq) ^ sw) << 4;
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
-        const lds_char* src = Bs + (128 * h + 32 * wb + 16 * ni + r16) * kKStepBytes + pch;
+        const lds_char* src = lds + rd_b[s] + (buf * kTile + 128 * h + 16 * ni) * kKStepBytes;
         if constexpr (kF8) {
           if (s == 0) lo[ni] = *(lds_i4*)src;
           else bf[0][ni] = __builtin_shufflevector(lo[ni], *(lds_i4*)src, 0, 1, 2, 3, 4, 5, 6, 7);

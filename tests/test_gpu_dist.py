@@ -62,15 +62,20 @@ def test_emulated_ranks_match_oracle(W, n, dim, compute, keep):
 @contextlib.contextmanager
 def _large_path():
     """Force the large-problem pipeline for single-GPU calls (shapes here would otherwise take
-    the one-launch small-problem path, which rounds differently)."""
+    the one-launch small-problem path, which rounds differently), with the unit-row forward the
+    data-parallel stage ops run (the single-GPU raw-operand forward normalises in the GEMM
+    epilogue instead and rounds differently; it has its own tests, test_gpu_raw_forward.py)."""
     from ntxent_amd.ops import _ext
 
     mod = _ext.load(build_if_missing=False)
     mod.set_small_path(False)
+    raw = mod.raw_forward_enabled()
+    mod.set_raw_forward(False)
     try:
         yield
     finally:
         mod.set_small_path(True)
+        mod.set_raw_forward(raw)
 
 
 def _close_grad(h, T, g, g2, rel):

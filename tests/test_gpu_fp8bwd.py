@@ -48,7 +48,15 @@ def test_fp8_backward_error_vs_oracle(ext, rows, dim, T):
           f"max|g8 - g16|/max|g16| {eb:.3e}")
     assert torch.isfinite(g8).all()
     assert not torch.equal(g8, g16)  # the e4m3 path ran
-    # e4m3 keeps 3 mantissa bits: a component dominated by a few large coefficients carries their
-    # ~3 % rounding (measured 5.0e-2 of max|g| at rows=4096, d=512, T=0.07)
-    assert eb <= 8e-2, eb
-    assert e8 <= e16 + 3e-2, (e8, e16)
+    # round 5: with the row scale taken from a bound on each row's largest negative (not the
+    # fixed-shift M), the e4m3 operands cost less than the bf16 rounding of the gradient itself
+    # (measured 5.3e-3 at rows=4096, d=512; 5.8e-3 at 16384 x 1024: one bf16 ulp of the largest
+    # component); round 4's M-based scale gave 5e-2. Verdict r4 item 7: within 2x of the fp16
+    # backward's error against the fp64 oracle.
+    assert eb <= 1.6e-2, eb
+    assert e8 <= 2 * e16 + 2e-3, (e8, e16)
+
+
+def test_fp8_backward_is_default(ext):
+    """FP8 plans take the e4m3 backward unless switched off (set_fp8_backward(False))."""
+    assert ext.fp8_backward_enabled()
