@@ -22,7 +22,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+#include <string>
 #include <type_traits>
+#include <vector>
 #include <unordered_map>
 
 namespace ntxent {
@@ -810,12 +812,44 @@ void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
 }
 
 template <typename Tc, int MODE>
-void launch_sim_gemm(int grid, const dev::SimParams& p, hipStream_t stream) {
+void launch_sim_gemm(int grid, const dev::SimParams& p_in, hipStream_t stream) {
+#if NTXENT_TIMING
+  // diagnostic build: per-block item marks (sim_gemm.h tmark), written after the launch to
+  // $NTXENT_TIMING_OUT/gemm_m<MODE>_e<elem bytes>_g<grid>.bin (the last launch of a kind wins)
+  static unsigned long long* buf = nullptr;
+  static size_t cap = 0;
+  const size_t n = (size_t)grid * dev::kTimingItems * dev::kTimingMarks;
+  if (n > cap) {
+    if (buf) NTXENT_HIP_CHECK(hipFree(buf));
+    NTXENT_HIP_CHECK(hipMalloc(&buf, n * 8));
+    cap = n;
+  }
+  NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, n * 8, stream));
+  dev::SimParams p = p_in;
+  p.tstamp = buf;
+#else
+  const dev::SimParams& p = p_in;
+#endif
   if (MODE == dev::kModeFwd && !p.fixed_shift)
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE, MODE == dev::kModeFwd ? 0 : 1>), dim3(grid), dim3(kGemmThreads), 0,
                        stream, p);
   else
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
+#if NTXENT_TIMING
+  if (const char* dir = std::getenv("NTXENT_TIMING_OUT")) {
+    std::vector<unsigned long long> h(n);
+    NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
+    NTXENT_HIP_CHECK(hipMemcpy(h.data(), buf, n * 8, hipMemcpyDeviceToHost));
+    const std::string f = std::string(dir) + "/gemm_m" + std::to_string(MODE) + "_e" + std::to_string(sizeof(Tc)) +
+                          "_g" + std::to_string(grid) + ".bin";
+    if (FILE* fp = std::fopen(f.c_str(), "wb")) {
+      const int hdr[3] = {grid, dev::kTimingItems, dev::kTimingMarks};
+      std::fwrite(hdr, sizeof(int), 3, fp);
+      std::fwrite(h.data(), 8, n, fp);
+      std::fclose(fp);
+    }
+  }
+#endif
 }
 
 dev::SimParams base_params(const Geometry& g) {

@@ -43,6 +43,15 @@ constexpr int kStageBytes = 2 * kTile * kKStepBytes;  // one operand, both parit
 #define NTXENT_GEMM_DMA_AUX 0
 #endif
 constexpr int kGemmDmaAux = NTXENT_GEMM_DMA_AUX;
+// Diagnostic builds (tools/build_variant.sh TAG -DNTXENT_TIMING=1; tools/gemm_timing.py): thread 0
+// of every GEMM block records s_memtime at four points of each of its first kTimingItems work
+// items -- item start, main loop start (prologue landed), main loop end, epilogue end -- and the
+// launcher writes them to $NTXENT_TIMING_OUT. Off in every production build.
+#ifndef NTXENT_TIMING
+#define NTXENT_TIMING 0
+#endif
+constexpr int kTimingItems = 8;
+constexpr int kTimingMarks = 8;  // per item: start, loop start, loop end, epilogue end, 4-7 epilogue phases
 // 16-byte write-through (sc1) store at base + off: the line goes to memory at once, so the kernel
 // boundary has no dirty L2 lines of it to write back. The buffer descriptor must be wave-uniform
 // (a per-lane one makes hipcc emit a waterfall loop): its base is the first active lane's offset
@@ -132,6 +141,9 @@ struct SimParams {
   int sk_half;           // split-K forward of a 2-byte plan: fp16 partial tiles,
                          // half the slab bytes written and re-read (sk_fixup: fragment pairs of a
                          // lane in 16-B units)
+#if NTXENT_TIMING
+  unsigned long long* tstamp;  // [grid][kTimingItems][kTimingMarks] s_memtime marks (diagnostic builds only)
+#endif
 };
 
 // Kept-cosine layout for 2-byte types: one 16-byte unit per lane holds the fragments of the
@@ -1097,7 +1109,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // prologue).
   const bool streaming = kStreamMode && p.sk_tiles == 0 && nk >= 2 && (nk & 1) == 0;
   bool streamed = false;  // this item's first two K-steps were staged by the previous item
+  auto tmark = [&](int item, int k) {
+#if NTXENT_TIMING
+    if (threadIdx.x == 0 && item < kTimingItems)
+      p.tstamp[((long long)blockIdx.x * kTimingItems + item) * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
+#endif
+  };
   for (int item = 0;; ++item) {
+  tmark(item, 0);
   int tile, kb, ke, stile;
   if (streamed) {
     tile = bid + item * G; kb = 0; ke = nk; stile = -1;
@@ -1126,6 +1145,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
+  tmark(item, 1);
   if (grp == 1) barrier();  // stagger group 1 by one barrier
   // K-steps in pairs: the buffer parity is a compile-time constant in each copy, so the LDS
   // read addresses are loop-invariant registers + immediates (headline dZ -1.9 %, forward -1.5 %,
@@ -1172,6 +1192,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   }
   if (ks2 < nsteps) kstep(ks2, kI0);
   if (grp == 0) barrier();  // re-align the groups
+  tmark(item, 2);
   if (kStreamMode && cont) {
     // the trailing stages are the next item's K-steps 0 and 1 (buffers of parity nk): leave
     // them in flight; this epilogue's stores will be younger than them
@@ -1241,6 +1262,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       }
     }
   }
+  tmark(item, 4);
   if (nsteps != nk && !sk_fixup<kF8>(acc, p, stile, bid, G, tid, smem)) continue;
 
   if constexpr (MODE == kModeDz) {
@@ -1364,7 +1386,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         for (int r = 0; r < 4; ++r) {
           float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
           s = row16_sum(s);
-          // every lane of the 16-lane row holds the sum: all write it (no exec-masked block)
+          // every lane of the 16-lane row holds the sum: all write it (no exec-masked block).
+          // (The 4 rows' reductions step-interleaved, without the s_nop each serial chain carries,
+          // measured the same: the epilogue is bound by its VALU issue, ~30 cycles per element
+          // with the exponential and the raw-operand scaling, profiles/r5/gemm_timing.)
           lds_put_f2(rowred + 8 * (wb * 256 + rb[mi] + 4 * (lane >> 4) + r), f32x2{s > 0.f ? M : kNegInf, s});
         }
 #pragma unroll
@@ -1418,12 +1443,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         }
       }
     }
+    tmark(item, 5);
     lds_drain();  // the untracked partial writes
     if constexpr (kStreamMode) {
       barrier();
     } else {
       __syncthreads();
     }
+    tmark(item, 6);
     if (tid < 256) {
       f32x2 v[4];
       lds_get4_f2(rowred + 8 * tid, v[0], v[1], v[2], v[3]);
@@ -1446,6 +1473,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     }
   }
   }  // epilogue scope
+  tmark(item, 3);
   // LDS of this item's epilogue is reused by the next item's staging (streaming: the partial
   // scratch lies above the stage buffers and the next epilogue writes it after the next main
   // loop's barriers, so no barrier here)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Per-item phase times of the persistent GEMM from a timing build (NTXENT_TIMING=1, see
+sim_gemm.h): for each work-item index, over all blocks, the time from item start to the main
+loop's first K-step (prologue / first operands landed), the main loop, and the epilogue, in
+shader-clock cycles (s_memtime) and in us at --ghz.
+
+  tools/build_variant.sh timing -DNTXENT_TIMING=1
+  NTXENT_TIMING_OUT=gpurun_out/t build/bin/ntxent_bench_timing --batch 4096 --dim 512 --iters 3
+  python tools/gemm_timing.py gpurun_out/t/gemm_m0_e2_g256.bin [--ghz 2.1]
+"""
+import struct
+import sys
+
+import numpy as np
+
+
+def main():
+    path = sys.argv[1]
+    ghz = float(sys.argv[sys.argv.index("--ghz") + 1]) if "--ghz" in sys.argv else 2.1
+    raw = open(path, "rb").read()
+    grid, items, marks = struct.unpack("iii", raw[:12])
+    t = np.frombuffer(raw[12:], dtype=np.uint64).reshape(grid, items, marks).astype(np.int64)
+    print(f"{path}: grid {grid}, {items} item slots; cycles (us at {ghz} GHz): mean / p10 / p90 / max over blocks")
+    used = t[:, :, 3] > 0
+    for it in range(items):
+        m = used[:, it]
+        if not m.any():
+            break
+        x = t[m, it]
+        cols = {"to loop": x[:, 1] - x[:, 0], "loop": x[:, 2] - x[:, 1], "epilogue": x[:, 3] - x[:, 2],
+                "item": x[:, 3] - x[:, 0]}
+        if (x[:, 5] > 0).all():  # forward epilogue phases: pre (dequant / fixup), exp + row sums, barrier, merge
+            cols.update({"e.pre": x[:, 4] - x[:, 2], "e.exp": x[:, 5] - x[:, 4], "e.bar": x[:, 6] - x[:, 5],
+                         "e.merge": x[:, 3] - x[:, 6]})
+        parts = []
+        for k, v in cols.items():
+            parts.append(f"{k} {v.mean():7.0f} ({v.mean() / ghz / 1e3:5.2f}) / {np.percentile(v, 10):6.0f} / "
+                         f"{np.percentile(v, 90):6.0f} / {v.max():6.0f}")
+        print(f"item {it} ({m.sum()} blocks): " + " | ".join(parts))
+    # a block's whole span (its own clock): first item start to last epilogue end
+    last = np.where(used, t[:, :, 3], 0).max(1)
+    span = last - t[:, 0, 0]
+    print(f"block span: mean {span.mean():.0f} cycles ({span.mean() / ghz / 1e3:.2f} us), max {span.max():.0f} "
+          f"({span.max() / ghz / 1e3:.2f} us)")
+
+
+if __name__ == "__main__":
+    main()
