@@ -126,6 +126,22 @@ __device__ __forceinline__ float row16_sum(float x) {
   x += dpp_f<0x121>(x);
   return x;
 }
+// Four rows' sums over the 16 lanes of a DPP row at once: x[r] holds this lane's part of row r;
+// returns the total of row (lane >> 2) & 3 (a transposing reduction: each exchange halves the
+// rows a lane carries, 5 DPP adds + 6 selects instead of 4 x 4 DPP adds). Partners: lane ^ 8
+// (row_ror:8), the half-row mirror (lane ^ 7 within 8), then ^ 1 and ^ 2 (quad_perm).
+__device__ __forceinline__ float row16_sum4t(const float (&x)[4], int lane) {
+  const bool b3 = (lane & 8) != 0, b2 = (lane & 4) != 0;
+  float ka = b3 ? x[2] : x[0], kb = b3 ? x[3] : x[1];  // rows kept: {0, 1} or {2, 3}
+  const float sa = b3 ? x[0] : x[2], sb = b3 ? x[1] : x[3];  // the partner's rows
+  ka += dpp_f<0x128>(sa);
+  kb += dpp_f<0x128>(sb);
+  float k = b2 ? kb : ka;
+  k += dpp_f<0x141>(b2 ? ka : kb);  // row_half_mirror
+  k += dpp_f<0xB1>(k);              // quad_perm [1, 0, 3, 2]
+  k += dpp_f<0x4E>(k);              // quad_perm [2, 3, 0, 1]
+  return k;
+}
 // Reduce across lanes l, l^16, l^32, l^48 (the 4 DPP rows).
 __device__ __forceinline__ float xrow_max(float x) {
   x = fmaxf(x, __shfl_xor(x, 16, 64));
@@ -161,6 +177,25 @@ __device__ __forceinline__ f32x4 lds_get_f32x4(unsigned addr) {
   f32x4 v;
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
   return v;
+}
+// the raw-operand forward's inverse norms of one item (sim_gemm_kernel epilogue): 4 column
+// values at cbase + {0, 64, 512, 576} and 4 row quads at rbase + {0, 64, 128, 192} + rofs, one
+// wait for all eight reads (a wait per read exposed ~1 k cycles of LDS latency per tile)
+template <int ROFS>
+__device__ __forceinline__ void lds_get_inv(unsigned rbase, unsigned cbase, f32x4 (&rs)[4], float (&cs)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %8 offset:%c10\n\t"
+      "ds_read_b128 %1, %8 offset:%c11\n\t"
+      "ds_read_b128 %2, %8 offset:%c12\n\t"
+      "ds_read_b128 %3, %8 offset:%c13\n\t"
+      "ds_read_b32 %4, %9\n\t"
+      "ds_read_b32 %5, %9 offset:64\n\t"
+      "ds_read_b32 %6, %9 offset:512\n\t"
+      "ds_read_b32 %7, %9 offset:576\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(rs[0]), "=&v"(rs[1]), "=&v"(rs[2]), "=&v"(rs[3]), "=&v"(cs[0]), "=&v"(cs[1]), "=&v"(cs[2]), "=&v"(cs[3])
+      : "v"(rbase), "v"(cbase), "i"(ROFS), "i"(ROFS + 64), "i"(ROFS + 128), "i"(ROFS + 192)
+      : "memory");
 }
 // four 8-byte reads at addr + {0, 1, 2, 3} * 2048
 __device__ __forceinline__ void lds_get4_f2(unsigned addr, f32x2& a, f32x2& b, f32x2& c, f32x2& d) {
@@ -230,6 +265,20 @@ __device__ __forceinline__ float block_sum(float x, float* red) {
   float t = 0.f;
   for (int i = 0; i < nw; ++i) t += red[i];  // fixed order: deterministic
   return t;
+}
+
+// Three block sums with one pair of barriers (same contract as block_sum; red: 3 * 8 floats).
+__device__ __forceinline__ void block_sum3(float& x, float& y, float& z, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nw = (blockDim.x + 63) >> 6;
+  x = wave_sum(x);
+  y = wave_sum(y);
+  z = wave_sum(z);
+  __syncthreads();
+  if (lane == 0) { red[w] = x; red[8 + w] = y; red[16 + w] = z; }
+  __syncthreads();
+  x = y = z = 0.f;
+  for (int i = 0; i < nw; ++i) { x += red[i]; y += red[8 + i]; z += red[16 + i]; }  // fixed order
 }
 
 // Block-wide max (same contract as block_sum).

@@ -247,17 +247,19 @@ __global__ __launch_bounds__(256) void prep_wave_kernel(const Tin* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ssi += a[c][j] * a[c][j]; ssp += b[c][j] * b[c][j]; }
   }
-  ssi = wave_sum(ssi);
-  ssp = wave_sum(ssp);
-  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
-  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  float hd = 0.f;  // statistics only: the pair's dot joins the two norms' reductions
   if constexpr (ST) {
-    float hd = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) hd += a[c][j] * b[c][j];
     hd = wave_sum(hd);
+  }
+  ssi = wave_sum(ssi);
+  ssp = wave_sum(ssp);
+  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
+  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
+  if constexpr (ST) {
     if (lane == 0) {
       inv[i] = ivi; inv[pi] = ivp;
       ypos[i] = hd * ivi * ivp * y_scale; ypos[pi] = ypos[i];
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
                                                          float* __restrict__ inv, float* __restrict__ ypos,
                                                          int R, int d, int dk, int ldk, float y_scale,
                                                          unsigned char* __restrict__ zq8, int dk8, int ldk8) {
-  __shared__ float red[16];
+  __shared__ float red[24];
   const int t = threadIdx.x;
   const int n = R >> 1, i = blockIdx.x, pi = i + n;
   if (i >= n) {  // pad row R + (i - n) of zq (and zq8): zeros
@@ -346,23 +348,25 @@ __global__ __launch_bounds__(256) void prep_block_kernel(const Tin* __restrict__
       if constexpr (Q8) { mxi = fmaxf(mxi, fabsf(a[c][j])); mxp = fmaxf(mxp, fabsf(b[c][j])); }
     }
   }
-  ssi = block_sum(ssi, red);
-  ssp = block_sum(ssp, red + 8);
-  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
-  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
-  if constexpr (ST) {  // statistics only (see prep_wave_kernel)
+  if constexpr (ST) {  // statistics only (see prep_wave_kernel): one reduction of the three sums
     float hd = 0.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) hd += a[c][j] * b[c][j];
-    hd = block_sum(hd, red);
+    block_sum3(ssi, ssp, hd, red);
+    const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
+    const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
     if (t == 0) {
       inv[i] = ivi; inv[pi] = ivp;
       ypos[i] = hd * ivi * ivp * y_scale; ypos[pi] = ypos[i];
     }
     return;
   }
+  ssi = block_sum(ssi, red);
+  ssp = block_sum(ssp, red + 8);
+  const float ivi = 1.0f / fmaxf(sqrtf(ssi), 1e-12f);
+  const float ivp = 1.0f / fmaxf(sqrtf(ssp), 1e-12f);
   int ei = 0, ep = 0;
   if constexpr (Q8) {
     ei = fp8_row_exp(block_max(mxi, red) * ivi);

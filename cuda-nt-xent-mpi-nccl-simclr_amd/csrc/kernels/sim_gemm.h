@@ -1249,17 +1249,20 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       // and retired by the main loop's counted waits and barriers (untracked reads: the next
       // item's DMA may be in flight)
       const unsigned ib = (unsigned)(uintptr_t)(lds + kInvLds) + (unsigned)((item & 1) * 2048);
-      float cs[4];
+      // (cb[ni] = cb[0] + {0, 16, 128, 144}, rb[mi] = rb[0] + 16 (mi & 3) + 128 (mi >> 2))
+      const unsigned rbase = ib + 4 * (rb[0] + 4 * (lane >> 4)), cbase = ib + 4 * (kTile + cb[0] + (lane & 15));
+      float cs[4], cs2[4];
+      f32x4 rs[4];
+      auto scale4 = [&](int m0) {
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) cs[ni] = lds_get_f32(ib + 4 * (kTile + cb[ni] + (lane & 15)));
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const f32x4 rs = lds_get_f32x4(ib + 4 * (rb[mi] + 4 * (lane >> 4)));
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[mi][ni][r] *= rs[r] * cs[ni];
-      }
+          for (int ni = 0; ni < 4; ++ni) acc[m0 + q][ni] *= rs[q] * cs[ni];
+      };
+      lds_get_inv<0>(rbase, cbase, rs, cs);
+      scale4(0);
+      lds_get_inv<512>(rbase, cbase, rs, cs2);
+      scale4(4);
     }
   }
   tmark(item, 4);
@@ -1275,6 +1278,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     // keep cosines (compact slot per tile, canonical order): the stores of 16-row block mi
     typedef typename StoreT<T>::type TS;
     TS* const st = p.sc ? reinterpret_cast<TS*>(p.sc) + (long long)tile * kTileElems : nullptr;
+    // the tile's 128 KiB slot as one buffer resource (wave-uniform base: store16_wt's per-store
+    // scalar base arithmetic is not needed inside one tile)
+    const auto st_rs = __builtin_amdgcn_make_buffer_rsrc(st, 0, 0x7FFFFFFF, 0x00020000);
     auto store_cos = [&](int mi) {
 #pragma unroll
       for (int np = 0; np < 2; ++np) {
@@ -1289,7 +1295,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           }
           // write-through: -1.1 % headline, -2.3 % config 2 fwd+bwd vs default-policy stores, config
           // 5 as the non-temporal form (profiles/r4/variants_r4_v7_wt.md)
-          store16_wt(st, (long long)sc_unit(rb[mi], cb[2 * np], lane) * 16, pk.u);
+          __builtin_amdgcn_raw_buffer_store_b128(pk.u, st_rs, sc_unit(rb[mi], cb[2 * np], lane) * 16, 0, 16);
         } else {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
@@ -1370,7 +1376,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       // Streamed per 16-row block: exponentiate (exp2(-inf) = 0 for the masked elements),
       // reduce the 4 rows, fold into the column sums; acc[mi] is dead afterwards, which keeps
       // the epilogue's register footprint at the accumulators'.
-      float csum[4] = {0.f, 0.f, 0.f, 0.f};
+      f32x2 csum2[4] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+      f32x2 sc2 = {sc_, sc_}, mM2 = {-M, -M};
+      asm volatile("" : "+v"(sc2), "+v"(mM2));  // VGPR pairs: the packed FMA's operands
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi) {
         // this block's cosine stores go out between the exponentials of the blocks: the CU's
@@ -1379,28 +1387,32 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         if (st) store_cos(mi);
         if (mask_any) mask_rows(mi);
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
+        for (int ni = 0; ni < 4; ++ni) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[mi][ni][r] = fast_exp2(acc[mi][ni][r] * sc_ - M);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float s = (acc[mi][0][r] + acc[mi][1][r]) + (acc[mi][2][r] + acc[mi][3][r]);
-          s = row16_sum(s);
-          // every lane of the 16-lane row holds the sum: all write it (no exec-masked block).
-          // (The 4 rows' reductions step-interleaved, without the s_nop each serial chain carries,
-          // measured the same: the epilogue is bound by its VALU issue, ~30 cycles per element
-          // with the exponential and the raw-operand scaling, profiles/r5/gemm_timing.)
-          lds_put_f2(rowred + 8 * (wb * 256 + rb[mi] + 4 * (lane >> 4) + r), f32x2{s > 0.f ? M : kNegInf, s});
+          for (int h2 = 0; h2 < 2; ++h2) {  // packed FMAs: two arguments per instruction
+            const f32x2 y = __builtin_elementwise_fma(f32x2{acc[mi][ni][2 * h2], acc[mi][ni][2 * h2 + 1]}, sc2, mM2);
+            acc[mi][ni][2 * h2] = fast_exp2(y[0]);
+            acc[mi][ni][2 * h2 + 1] = fast_exp2(y[1]);
+          }
+        }
+        {
+          // row sums of the block's 4 rows (packed adds over the column blocks, one transposing
+          // 16-lane reduction, one LDS write per lane: lane holds row (lane >> 2) & 3), then the
+          // column partials as packed pairs
+          const f32x4 rsum = (acc[mi][0] + acc[mi][1]) + (acc[mi][2] + acc[mi][3]);
+          const float s4[4] = {rsum[0], rsum[1], rsum[2], rsum[3]};
+          const float s = row16_sum4t(s4, lane);
+          lds_put_f2(rowred + 8 * (wb * 256 + rb[mi] + 4 * (lane >> 4) + ((lane >> 2) & 3)), f32x2{s > 0.f ? M : kNegInf, s});
         }
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          csum[ni] += (acc[mi][ni][0] + acc[mi][ni][1]) + (acc[mi][ni][2] + acc[mi][ni][3]);
+          csum2[ni] += f32x2{acc[mi][ni][0], acc[mi][ni][1]} + f32x2{acc[mi][ni][2], acc[mi][ni][3]};
         __builtin_amdgcn_sched_barrier(0);  // keep the blocks streamed (no hoisted exps to spill)
       }
       if (col_out) {
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
-          const float s = xrow_sum(csum[ni]);
+          const float s = xrow_sum(csum2[ni][0] + csum2[ni][1]);
           lds_put_f2(colred + 8 * (wa * 256 + cb[ni] + (lane & 15)), f32x2{s > 0.f ? M : kNegInf, s});
         }
       }
