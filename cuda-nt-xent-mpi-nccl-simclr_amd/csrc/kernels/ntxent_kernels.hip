@@ -815,22 +815,46 @@ void set_operand_scales(dev::SimParams& p, DType comp, const Geometry& g) {
   p.scale_off = comp == DType::FP8 ? g.dim_k8 : 0;
 }
 
+#if NTXENT_TIMING
+// Diagnostic builds: a device buffer of [grid][kTimingItems][kTimingMarks] s_memtime marks per
+// launch kind, written after the launch to $NTXENT_TIMING_OUT/<name>_g<grid>.bin (the last launch
+// of a kind wins; tools/gemm_timing.py reads them).
+struct TimingBuf {
+  unsigned long long* buf = nullptr;
+  size_t cap = 0, n = 0;
+  unsigned long long* prepare(int grid, hipStream_t stream) {
+    n = (size_t)grid * dev::kTimingItems * dev::kTimingMarks;
+    if (n > cap) {
+      if (buf) NTXENT_HIP_CHECK(hipFree(buf));
+      NTXENT_HIP_CHECK(hipMalloc(&buf, n * 8));
+      cap = n;
+    }
+    NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, n * 8, stream));
+    return buf;
+  }
+  void dump(const std::string& name, int grid, hipStream_t stream) const {
+    const char* dir = std::getenv("NTXENT_TIMING_OUT");
+    if (!dir) return;
+    std::vector<unsigned long long> h(n);
+    NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
+    NTXENT_HIP_CHECK(hipMemcpy(h.data(), buf, n * 8, hipMemcpyDeviceToHost));
+    const std::string f = std::string(dir) + "/" + name + "_g" + std::to_string(grid) + ".bin";
+    if (FILE* fp = std::fopen(f.c_str(), "wb")) {
+      const int hdr[3] = {grid, dev::kTimingItems, dev::kTimingMarks};
+      std::fwrite(hdr, sizeof(int), 3, fp);
+      std::fwrite(h.data(), 8, n, fp);
+      std::fclose(fp);
+    }
+  }
+};
+#endif
+
 template <typename Tc, int MODE>
 void launch_sim_gemm(int grid, const dev::SimParams& p_in, hipStream_t stream) {
 #if NTXENT_TIMING
-  // diagnostic build: per-block item marks (sim_gemm.h tmark), written after the launch to
-  // $NTXENT_TIMING_OUT/gemm_m<MODE>_e<elem bytes>_g<grid>.bin (the last launch of a kind wins)
-  static unsigned long long* buf = nullptr;
-  static size_t cap = 0;
-  const size_t n = (size_t)grid * dev::kTimingItems * dev::kTimingMarks;
-  if (n > cap) {
-    if (buf) NTXENT_HIP_CHECK(hipFree(buf));
-    NTXENT_HIP_CHECK(hipMalloc(&buf, n * 8));
-    cap = n;
-  }
-  NTXENT_HIP_CHECK(hipMemsetAsync(buf, 0, n * 8, stream));
+  static TimingBuf tb;
   dev::SimParams p = p_in;
-  p.tstamp = buf;
+  p.tstamp = tb.prepare(grid, stream);
 #else
   const dev::SimParams& p = p_in;
 #endif
@@ -840,19 +864,7 @@ void launch_sim_gemm(int grid, const dev::SimParams& p_in, hipStream_t stream) {
   else
     hipLaunchKernelGGL((dev::sim_gemm_kernel<Tc, MODE>), dim3(grid), dim3(kGemmThreads), 0, stream, p);
 #if NTXENT_TIMING
-  if (const char* dir = std::getenv("NTXENT_TIMING_OUT")) {
-    std::vector<unsigned long long> h(n);
-    NTXENT_HIP_CHECK(hipStreamSynchronize(stream));
-    NTXENT_HIP_CHECK(hipMemcpy(h.data(), buf, n * 8, hipMemcpyDeviceToHost));
-    const std::string f = std::string(dir) + "/gemm_m" + std::to_string(MODE) + "_e" + std::to_string(sizeof(Tc)) +
-                          "_g" + std::to_string(grid) + ".bin";
-    if (FILE* fp = std::fopen(f.c_str(), "wb")) {
-      const int hdr[3] = {grid, dev::kTimingItems, dev::kTimingMarks};
-      std::fwrite(hdr, sizeof(int), 3, fp);
-      std::fwrite(h.data(), 8, n, fp);
-      std::fclose(fp);
-    }
-  }
+  tb.dump("gemm_m" + std::to_string(MODE) + "_e" + std::to_string(sizeof(Tc)), grid, stream);
 #endif
 }
 
@@ -1385,6 +1397,10 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // row-group partials in the column-partial area of the workspace
         float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                     (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
+#if NTXENT_TIMING
+        static TimingBuf tb;
+        q.tstamp = tb.prepare(nstrip * (diag_ks(nk_tile) == 2 ? dev::diag_up_blocks<2>() : dev::diag_up_blocks<1>()), stream);
+#endif
         if (diag_ks(nk_tile) == 2) {
           const dim3 sg(nstrip * dev::diag_up_blocks<2>());
           if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q, scratch);
@@ -1394,6 +1410,9 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
           if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1>), sg, dim3(256), 0, stream, q, scratch);
           else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1>), sg, dim3(256), 0, stream, q, scratch);
         }
+#if NTXENT_TIMING
+        tb.dump("diag_up", nstrip * (diag_ks(nk_tile) == 2 ? dev::diag_up_blocks<2>() : dev::diag_up_blocks<1>()), stream);
+#endif
       }
     }
   });

@@ -1572,9 +1572,20 @@ constexpr int kSubStages = 3;
 // fp32 partials go to write-through slabs and the last piece to arrive (ticket) sums them in piece
 // order. 4 + 10 tickets and 10 KS 16 KiB slabs per tile (launch_fwd_stats checks the workspace).
 constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + column-partial exchange + flags
-template <int KS> constexpr int diag_up_blocks() { return 4 * (KS / 2 > 1 ? KS / 2 : 1) + 6 * KS; }
+// (diagonal regions in KS pieces as well: remainder 15.2 -> 16.4 us at the headline, the extra
+// piece merges cost more than the shorter K loop saves: profiles/r5/gemm_timing/diag_up.md)
+template <int KS> constexpr int diag_ksd() { return KS / 2 > 1 ? KS / 2 : 1; }
+template <int KS> constexpr int diag_up_blocks() { return 4 * diag_ksd<KS>() + 6 * KS; }
 template <typename T, int FX, int KS>
 __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch) {
+#if NTXENT_TIMING
+  auto dmark = [&](int k) {
+    if (threadIdx.x == 0) p.tstamp[(long long)blockIdx.x * kTimingItems * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
+  };
+#else
+  auto dmark = [](int) {};
+#endif
+  dmark(0);
   using MM = Mfma<T>;
   typedef typename MM::frag frag;
   typedef typename StoreT<T>::type TS;
@@ -1583,7 +1594,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   lds_char* lds = (lds_char*)smem;
   // scalar wave index (scalar M0 arithmetic for the DMA pieces, as sim_gemm_kernel: -0.3 us)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int KSD = KS / 2 > 1 ? KS / 2 : 1;        // K pieces of a diagonal region
+  constexpr int KSD = diag_ksd<KS>();                  // K pieces of a diagonal region
   constexpr int NB = diag_up_blocks<KS>();            // blocks per tile
   const int nt_d = gridDim.x / NB;                    // diagonal tiles in this launch
   const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's blocks share one XCD
@@ -1629,6 +1640,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   for (int f = 0; f < 4; ++f) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int P = NSt - 1;  // K-steps in flight: 5 (diagonal region) or 2
   for (int i = 0; i < P; ++i) stage(k0 + i < k1 ? k0 + i : k1 - 1, i);
+  dmark(1);
   int buf = 0;
   for (int st = k0; st < k1; ++st) {
     // own pieces of step st landed (the P - 1 younger steps' np each in flight: 2 x 4 or 4 x 1);
@@ -1658,6 +1670,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
     buf = buf == NSt - 1 ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing prefetches
+  dmark(2);
   if (p.inv_a) {  // raw operands: normalise (lane: rows 64a + 16w + 4 (lane >> 4) + r, cols 64b + 16f + (lane & 15))
     const f32x4 rs = *reinterpret_cast<const f32x4*>(p.inv_a + (long long)mt * kTile + 64 * a + 16 * w + 4 * (lane >> 4));
 #pragma unroll
@@ -1704,6 +1717,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
 #pragma unroll
     for (int f = 0; f < 4; ++f) acc[f] = sum[f];
   }
+  dmark(3);
   // lane holds S[row 64a + 16w + 4 (lane >> 4) + r][col 64b + 16 f + (lane & 15)] (tile-local)
   const int rb0 = 64 * a + 16 * w;
   if (p.sc) {  // kept cosines of region (a, b), canonical fragment order, before the masks
@@ -1783,8 +1797,10 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
       __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(m), __float_as_uint(sm)}, crs, (a * 64 + tid) * 8, 0, 16);
     }
   }
+  dmark(4);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  dmark(5);
   if (tid == 0) {  // one ticket per contributed row group; the 4th contributor merges the group
     int lastm = 0;
     const int ga[2] = {a, b};
@@ -1799,6 +1815,7 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   }
   __syncthreads();
   const int lastm = flag[1];
+  dmark(6);
   const int k = tid >> 6;  // wave 0 merges group a, wave 1 group b
   if (k > 1 || !((lastm >> k) & 1)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket

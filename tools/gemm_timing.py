@@ -20,6 +20,8 @@ def main():
     raw = open(path, "rb").read()
     grid, items, marks = struct.unpack("iii", raw[:12])
     t = np.frombuffer(raw[12:], dtype=np.uint64).reshape(grid, items, marks).astype(np.int64)
+    if "diag_up" in path:
+        return diag_up(t[:, 0, :], grid, ghz, path)
     print(f"{path}: grid {grid}, {items} item slots; cycles (us at {ghz} GHz): mean / p10 / p90 / max over blocks")
     used = t[:, :, 3] > 0
     for it in range(items):
@@ -42,6 +44,25 @@ def main():
     span = last - t[:, 0, 0]
     print(f"block span: mean {span.mean():.0f} cycles ({span.mean() / ghz / 1e3:.2f} us), max {span.max():.0f} "
           f"({span.max() / ghz / 1e3:.2f} us)")
+
+
+def diag_up(x, grid, ghz, path):
+    """diag_up_kernel marks: 0 start, 1 ring prologue issued, 2 K loop done, 3 K pieces merged
+    (last piece only), 4 epilogue stores issued, 5 drained, 6 past the row-group ticket."""
+    print(f"{path}: grid {grid}; ticks (us at {ghz} GHz): mean / p50 / p90 / max over the blocks that reach each mark")
+    names = ["prologue", "K loop", "piece merge", "epilogue", "drain", "ticket"]
+    for k, nm in enumerate(names):
+        m = (x[:, k + 1] > 0) & (x[:, k] > 0)
+        if not m.any():
+            continue
+        v = x[m, k + 1] - x[m, k]
+        print(f"  {nm:12s} ({m.sum():4d} blocks): {v.mean():8.0f} ({v.mean() / ghz / 1e3:5.2f}) / {np.median(v):7.0f} / "
+              f"{np.percentile(v, 90):7.0f} / {v.max():7.0f}")
+    last = x.max(1)
+    span = last - x[:, 0]
+    print(f"  block span: mean {span.mean():.0f} ({span.mean() / ghz / 1e3:.2f} us), max {span.max():.0f}; "
+          f"start spread (if clocks agree) {(x[:, 0].max() - x[:, 0].min()) / ghz / 1e3:.2f} us, "
+          f"first start to last mark {(last.max() - x[:, 0].min()) / ghz / 1e3:.2f} us")
 
 
 if __name__ == "__main__":
