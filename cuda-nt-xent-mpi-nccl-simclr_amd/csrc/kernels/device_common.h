@@ -197,6 +197,32 @@ __device__ __forceinline__ void lds_get_inv(unsigned rbase, unsigned cbase, f32x
       : "v"(rbase), "v"(cbase), "i"(ROFS), "i"(ROFS + 64), "i"(ROFS + 128), "i"(ROFS + 192)
       : "memory");
 }
+// fp8 operand row scales of one item (sim_gemm_kernel): 8 A dwords at abase + {0, 64, 128, 192,
+// 512, 576, 640, 704} and 4 B dwords at bbase + {0, 64, 512, 576}, one wait
+__device__ __forceinline__ void lds_get_scales(unsigned abase, unsigned bbase, unsigned (&av)[8], unsigned (&bv)[4]) {
+  asm volatile(
+      "ds_read_b32 %0, %12\n\t"
+      "ds_read_b32 %1, %12 offset:64\n\t"
+      "ds_read_b32 %2, %12 offset:128\n\t"
+      "ds_read_b32 %3, %12 offset:192\n\t"
+      "ds_read_b32 %4, %12 offset:512\n\t"
+      "ds_read_b32 %5, %12 offset:576\n\t"
+      "ds_read_b32 %6, %12 offset:640\n\t"
+      "ds_read_b32 %7, %12 offset:704\n\t"
+      "ds_read_b32 %8, %13\n\t"
+      "ds_read_b32 %9, %13 offset:64\n\t"
+      "ds_read_b32 %10, %13 offset:512\n\t"
+      "ds_read_b32 %11, %13 offset:576\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(av[0]), "=&v"(av[1]), "=&v"(av[2]), "=&v"(av[3]), "=&v"(av[4]), "=&v"(av[5]), "=&v"(av[6]),
+        "=&v"(av[7]), "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+      : "v"(abase), "v"(bbase)
+      : "memory");
+}
+// low bytes of four dwords packed into one (byte i = low byte of x[i])
+__device__ __forceinline__ int pack_low_bytes(unsigned x0, unsigned x1, unsigned x2, unsigned x3) {
+  return (int)((x0 & 0xffu) | ((x1 & 0xffu) << 8) | ((x2 & 0xffu) << 16) | ((x3 & 0xffu) << 24));
+}
 // four 8-byte reads at addr + {0, 1, 2, 3} * 2048
 __device__ __forceinline__ void lds_get4_f2(unsigned addr, f32x2& a, f32x2& b, f32x2& c, f32x2& d) {
   asm volatile(

@@ -907,10 +907,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(lds + kInvLds + slot * 2048 + 256 * w), 4, 0, 0);
     }
   };
-  // fp8: the MFMA runs with unit E8M0 scales (127); the rows' power-of-two scales are applied to
-  // the accumulators before the epilogue (exact). Per-lane scale operands loaded per tile cost a
-  // vmcnt(0) drain of the prologue DMA (a plain load's first use with LDS-DMA in flight).
+  // fp8: the block-scaled MFMA applies the rows' power-of-two E8M0 scales itself (exact): per
+  // item, each lane packs the scale bytes of its 8 A row blocks (byte mi of sa_v[h]) and 4 B
+  // column blocks (byte i of sb_v) from the prologue's LDS copy, read by untracked LDS reads after
+  // the first counted wait (a plain global load there made hipcc drain the prologue DMA). Round 4
+  // ran unit scales and multiplied the accumulators in the epilogue (-1.5 k cycles per item).
+  // The dZ's C and Z^T carry no E8M0 scales (unit; per-row dequantisation in dz8_finish).
   const int kUnitScale = 0x7f7f7f7f;
+  int sa_v[2] = {kUnitScale, kUnitScale}, sb_v = kUnitScale;
 
   const int r16 = lane & 15, sw = (r16 >> 1) & 7, cq = lane >> 4;
   // Operand registers [k-substep][block]. fp8: ONE 32-byte register set per block holding both
@@ -979,7 +983,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         if constexpr (MODE == kModeDz)
           c = mma_mx_c<qb * 2 + ni, mi>(bf[0][ni], af[0][mi], c, kUnitScale, kUnitScale);
         else
-          c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, kUnitScale, kUnitScale);
+          c = mma_mx_c<mi, qb * 2 + ni>(af[0][mi], bf[0][ni], c, sa_v[qa], sb_v);
         // The block-scaled MFMA intrinsic is not convergent, so LLVM's IR sinking moved every
         // cluster of a K-step into the loop latch (one 32-MFMA cluster, operands of all phases
         // live at once -> spills and a vmcnt(0) in the loop). An empty asm use pins it here.
@@ -1145,6 +1149,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
+  if constexpr (kF8 && MODE != kModeDz) {  // this item's scale bytes (landed with A0(0), B0(0))
+    const int r16_ = lane & 15;
+    unsigned av[8], bv[4];
+    lds_get_scales((unsigned)(uintptr_t)(lds + kScaleLds) + 4 * (64 * wa + r16_),
+                   (unsigned)(uintptr_t)(lds + kScaleLds) + 4 * (256 + 32 * wb + r16_), av, bv);
+    sa_v[0] = pack_low_bytes(av[0], av[1], av[2], av[3]);
+    sa_v[1] = pack_low_bytes(av[4], av[5], av[6], av[7]);
+    sb_v = pack_low_bytes(bv[0], bv[1], bv[2], bv[3]);
+  }
   tmark(item, 1);
   if (grp == 1) barrier();  // stagger group 1 by one barrier
   // K-steps in pairs: the buffer parity is a compile-time constant in each copy, so the LDS
@@ -1201,27 +1214,6 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     streamed = false;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the trailing (clamped) prefetches
   }
-  if constexpr (kF8 && MODE != kModeDz) {
-    // dequantise: acc(i, j) * 2^-e_i * 2^-e_j, exact, before any stream-K sum (acc row = rb +
-    // 4 (lane >> 4) + r: four consecutive scale dwords; column = cb + (lane & 15))
-    typedef __attribute__((address_space(3))) const unsigned lds_u32;
-    typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
-    float cf[4];
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      cf[ni] = e8m0_to_f32((unsigned char)*(lds_u32*)(lds + kScaleLds + 4 * (256 + 128 * (ni >> 1) + 32 * wb + 16 * (ni & 1) + (lane & 15))));
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const u32x4 e4 = *(lds_u32x4*)(lds + kScaleLds + 4 * (128 * (mi >> 2) + 64 * wa + 16 * (mi & 3) + 4 * (lane >> 4)));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float rf = e8m0_to_f32((unsigned char)e4[r]);
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) acc[mi][ni][r] *= rf * cf[ni];
-      }
-    }
-  }
-
   if constexpr (kStreamMode) {
     lds_drain();  // raw barrier: a __syncthreads would drain the next item's DMA
     barrier();
