@@ -186,6 +186,12 @@ __device__ __forceinline__ int ct_swz(int L) {
   return ((L >> 1) & 1) | ((L & 1) << 1) | (((L >> 3) & 1) << 2) | ((((L >> 1) ^ (L >> 2)) & 1) << 3);
 }
 
+// A dot partial slot (coefficient pass; read by dot_reduce_kernel in the next launch). (Folding
+// that reduction into this launch -- each 64-row group's last contributing wave sums its slots,
+// found by an agent-scope ticket -- measured 42 -> 64 us for the pass at the headline: every
+// wave waits for its ticket's return under contention. profiles/r5/coef_dot/.)
+__device__ __forceinline__ void dot_slot_store(float* p, float v) { *p = v; }
+
 // Tile index of coefficient tile (mt, nt) in cbuf (row-major [row_tiles][c_ld] tiles).
 __device__ __forceinline__ long long ctile_index(const SimParams& p, int mt, int nt) {
   const int cs = p.c_rot ? (nt - p.row_tile0 + p.col_tiles) % p.col_tiles : nt - p.c_tile0;
@@ -255,6 +261,9 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   auto hits = [&](int a0) { return a0 < c_hi && c_lo < a0 + NROWS; };
   const bool plain = fixed && r_hi <= p.R && col_local0 + col_base + NCOLS <= p.R && !hits(p.own0 + r_lo) &&
                      !hits(p.own0 + r_lo + p.n_half) && !hits(p.own0 + r_lo - p.n_half);
+  // (row LSEs of all blocks loaded up front and the dot partials stored after the block loop,
+  // one transposing reduction per 4 rows: the pass measured 42 -> 44 us at the headline and
+  // 149 -> 154 us at config 5, not kept; the e4m3 epilogue below gains from the same change)
 #pragma unroll
   for (int mi = 0; mi < NMI; ++mi) {
     float c[4][4];
@@ -297,7 +306,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
         for (int ni = 0; ni < 4; ++ni) d += to_f32<T>(from_f32<T>(c[ni][r])) * acc[mi][ni][r];
         d = row16_sum(d);
         const int row = mt * kTile + rb[mi] + 4 * (lane >> 4) + r;
-        if ((lane & 15) == 0) p.dotp[(long long)(nt * 4 + wq) * p.Rpad + row] = d;
+        if ((lane & 15) == 0) dot_slot_store(p.dotp + (long long)(nt * 4 + wq) * p.Rpad + row, d);
       }
       const int h2 = NMI == 8 ? (mi >> 2) : 0;
 #pragma unroll
@@ -335,7 +344,7 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
           const float d = xrow_sum(cdot[h2][ni]);
           const int rq = NMI == 8 ? 2 * h2 + wa8 : (row_base >> 6);  // row quarter of this wave's rows
           const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
-          if (lane < 16) p.dotp[(long long)((p.row_tile0 + mt) * 4 + rq) * p.Rpad + row] = d;
+          if (lane < 16) dot_slot_store(p.dotp + (long long)((p.row_tile0 + mt) * 4 + rq) * p.Rpad + row, d);
         }
     }
   }
@@ -430,7 +439,7 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   const bool fixed = p.fixed_shift != 0;
   const float M = p.y_scale;
   const float lmin = p.q8_lmin[0];
-  float lcol[4], scol[4];
+  float lcol[4], scol[4], icol[4];
   bool cvalid[4];
   int gj[4];
 #pragma unroll
@@ -440,8 +449,11 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
     const float l = p.lse2[gj[ni]];
     lcol[ni] = fixed ? fast_exp2(M - l) : l;
     cvalid[ni] = (col_local0 + col_t) < p.R;
-    scol[ni] = exp2i(q8_row_exp(p.q8_mneg[gj[ni]], lmin));
+    const int e = q8_row_exp(p.q8_mneg[gj[ni]], lmin);
+    scol[ni] = exp2i(e);
+    icol[ni] = exp2i(-e);
   }
+  float dsv[4];  // row partial of row (lane >> 2) & 3 of each 4-row block (stored after the loop)
   // plain region: as coef_epilogue
   const int r_lo = mt * kTile + row_base, r_hi = r_lo + 64;
   const int c_lo = nt * kTile + col_base, c_hi = c_lo + 64;
@@ -455,12 +467,19 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
   const int qd = lane & 3;
   const unsigned sel1 = qd < 2 ? 0x05040100u : 0x03020706u;
   const unsigned sel2 = (qd & 1) ? 0x03070105u : 0x06020400u;
+  f32x4 lrow_h[4], mneg_h[4];  // loaded up front (as coef_epilogue)
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int gi0 = mt * kTile + rb[mi] + 4 * (lane >> 4);
+    lrow_h[mi] = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
+    mneg_h[mi] = *reinterpret_cast<const f32x4*>(p.q8_mneg + p.own0 + gi0);
+  }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
     const int row_t0 = rb[mi] + 4 * (lane >> 4);
     const int gi0 = mt * kTile + row_t0;
-    const f32x4 lrow4 = *reinterpret_cast<const f32x4*>(p.lse2 + p.own0 + gi0);
-    const f32x4 mneg4 = *reinterpret_cast<const f32x4*>(p.q8_mneg + p.own0 + gi0);
+    const f32x4 lrow4 = lrow_h[mi];
+    const f32x4 mneg4 = mneg_h[mi];
     float srow[4], lrow[4], rdot[4] = {0.f, 0.f, 0.f, 0.f}, rposd[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -510,19 +529,25 @@ __device__ __forceinline__ void coef_epilogue_q8(f32x4 (&acc)[4][4], const int (
                                                     (row_t0 - row_base)) = w_m;
     }
     if (p.dotp) {
+      float dd[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float d = row16_sum(fmaf(rdot[r], exp2i(-q8_row_exp(mneg4[r], lmin)), rposd[r]));
-        if ((lane & 15) == 0) p.dotp[(long long)(nt * 4 + wq) * p.Rpad + gi0 + r] = d;
-      }
+      for (int r = 0; r < 4; ++r) dd[r] = fmaf(rdot[r], exp2i(-q8_row_exp(mneg4[r], lmin)), rposd[r]);
+      dsv[mi] = row16_sum4t(dd, lane);
     }
+  }
+  if (p.dotp) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+      if ((lane & 3) == 0)
+        dot_slot_store(p.dotp + (long long)(nt * 4 + wq) * p.Rpad + mt * kTile + rb[mi] + 4 * (lane >> 4) + ((lane >> 2) & 3),
+                       dsv[mi]);
   }
   if (p.dotp && mirrored) {
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      const float d = xrow_sum(fmaf(cdot[ni], exp2i(-q8_row_exp(p.q8_mneg[gj[ni]], lmin)), cposd[ni]));
+      const float d = xrow_sum(fmaf(cdot[ni], icol[ni], cposd[ni]));
       const int row = (nt - p.row_tile0) * kTile + cb[ni] + (lane & 15);
-      if (lane < 16) p.dotp[(long long)((p.row_tile0 + mt) * 4 + (row_base >> 6)) * p.Rpad + row] = d;
+      if (lane < 16) dot_slot_store(p.dotp + (long long)((p.row_tile0 + mt) * 4 + (row_base >> 6)) * p.Rpad + row, d);
     }
   }
   __syncthreads();
@@ -1876,7 +1901,8 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float
       hoff[jp] = (unsigned)((((u >> 7) << 6) + (u & 63)) * 16);
     }
     const char* hs = reinterpret_cast<const char*>(p.sk_slabs);
-    for (int bb = b0; bb <= b1; bb += 4) {  // 8 loads in flight (clamped, weighted as below)
+    // 8 loads in flight (clamped, weighted as below; 16 measured +0.9 us at config 4)
+    for (int bb = b0; bb <= b1; bb += 4) {
       u32x4 x[4][2];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
