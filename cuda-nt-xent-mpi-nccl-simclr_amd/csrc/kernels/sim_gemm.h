@@ -1052,6 +1052,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // item's first counted waits stricter (vmcnt: all but the N youngest), so they drain under
   // the exponentials and the first phases. (Waits relaxed by the store count for those phases
   // measured slower: the per-phase selection cost more than the stores' drain.)
+  // (fp8 forward streamed as well, its scale bytes in two LDS slots staged one item ahead:
+  // config 5 fp8 forward 182-184 -> 188-189 us, not kept: profiles/r5/README.md)
   constexpr bool kStreamMode = MODE == kModeFwd && !kF8;
   // DMA wait, issued one phase AHEAD of the read it protects: the half-tile read in the NEXT
   // phase has retired for this wave (4 younger half-tiles may stay in flight).
