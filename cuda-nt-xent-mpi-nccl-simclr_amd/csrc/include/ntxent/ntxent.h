@@ -205,15 +205,21 @@ struct BlockView {
 // fp16) and normalises in its epilogue (cos = acc inv_i inv_j), the LSE launch transposes h * inv
 // into Z^T, and the row prologue only computes inv and the positive logits (launch_prep with
 // zq = null): no zq rows are written or read (prep 32 MiB lighter at the headline).
+// zqt (optional): launch_fwd_stats writes Z^T = (h inv)^T there itself when the launch has a
+// diagonal remainder (side blocks of diag_up_kernel, which is load-latency-bound on one block per
+// CU) and returns true; the LSE launch then only merges. Otherwise launch_lse transposes.
 struct RawRows {
   const void* h = nullptr;      // [rows][dim] input rows
   DType in = DType::BF16;       // their dtype (F16 or BF16)
   const float* inv = nullptr;   // [rows] 1 / |h_i|
+  void* zqt = nullptr;          // [dim_n][ld_t] Z^T in `zt` (the plan's backward dtype), or null
+  DType zt = DType::F16;
 };
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp);  // world 1, 2-byte in & comp, rows % 256, dim % 64
 void set_raw_forward(bool on);  // default on (off: the zq path, for A/B and tests)
 bool raw_forward_enabled();
-void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
+// Returns true when it wrote raw->zqt.
+bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all,
                       const int4* tiles, int ntiles, float2* part, void* sc,
                       const GemmWorkspace& ws, const Geometry& g, hipStream_t stream,
                       const BlockView& bv = BlockView{}, float2* part_x = nullptr,

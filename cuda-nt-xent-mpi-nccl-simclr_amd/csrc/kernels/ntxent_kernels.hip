@@ -448,6 +448,28 @@ __device__ __forceinline__ void transpose_tile(const Ts* __restrict__ zq, T* __r
   }
 }
 
+// Z^T = (h inv)^T of the raw-operand forward as the diagonal remainder's side job (diag_up_kernel
+// blocks [nup, grid)): 64x64 tiles strided over the side blocks, in 9 KiB of that kernel's LDS.
+// (Pairs of tiles per iteration, all four 16-B loads of a thread in flight: the remainder's
+// blocks slowed more, headline launch 18.4 -> 20.3 us: profiles/r5/zt_side/.)
+template <typename T, typename Ts>
+struct DiagSideZt {
+  int nup;
+  const Ts* h;
+  T* zqt;
+  const float* inv;
+  int dk, ldt, tx, ntiles;
+  __device__ void operator()(int b, int nb, char* smem) const {
+    typedef T Tile[64][64 + 16 / sizeof(T)];
+    static_assert(sizeof(Tile) <= kUpLds, "Z^T side job: tile exceeds the remainder's LDS");
+    Tile& tile = *reinterpret_cast<Tile*>(smem);
+    for (int t = b; t < ntiles; t += nb) {
+      transpose_tile<T, Ts>(h, zqt, dk, dk, ldt, t % tx, t / tx, tile, inv);
+      __syncthreads();  // every wave's gathers done before the next tile's rows land
+    }
+  }
+};
+
 // fp8 backward operand: e4m3(256 Z^T) ([dim_n][ldt] bytes) from the fp16 rows, same tiling (the
 // gathered 8 elements go out as one 8-byte store). |z| <= 1, so 256 z stays below the e4m3 max.
 __device__ __forceinline__ void transpose_tile_q8(const _Float16* __restrict__ zq, unsigned char* __restrict__ zqt,
@@ -1276,6 +1298,10 @@ bool fp8_backward_eligible(const Geometry& g, DType comp) { return comp == DType
 // MFMA busy 17 %: profiles/r5/fp8_dz)
 int q8_ldt(const Geometry& g) { return (!NTXENT_NO_LDPAD && g.rows_pad % 1024 == 0) ? g.rows_pad + 128 : g.rows_pad; }
 
+#ifndef NTXENT_ZT_SIDE_PER_CU
+#define NTXENT_ZT_SIDE_PER_CU 2  // Z^T side blocks of the diagonal remainder per CU (experiment builds: 1)
+#endif
+
 // K pieces of the diagonal remainder's off-diagonal regions (diag_up_kernel): 2 from 32 K-steps
 // up (the headline: 1 piece +2 us), 1 below (config 2 -1.5 us, config 5 -0.4 us:
 // profiles/r4/variants_r4_v29_diagks1.md; 4 pieces measured +6 us at config 5,
@@ -1299,11 +1325,12 @@ int fwd_splitk_pieces(int ntiles, int nk, int cus, int diag_tail) {
   return pcs >= 2 ? pcs : 0;
 }
 
-void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
+bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, const int4* tiles,
                       int ntiles, float2* part, void* sc, const GemmWorkspace& ws, const Geometry& g,
                       hipStream_t stream, const BlockView& bv, float2* part_x, int diag_tail,
                       hipEvent_t main_done, const RawRows* raw) {
-  if (ntiles == 0) return;
+  if (ntiles == 0) return false;
+  bool zt_done = false;  // raw->zqt written beside the diagonal remainder
   NTXENT_CHECK(diag_tail >= 0 && diag_tail <= ntiles, "fwd_stats: bad diagonal tail");
   const bool f8 = comp == DType::FP8;  // fp8: K = dim_k8 bytes of rows ld_k8 bytes apart
   if (raw) {
@@ -1397,26 +1424,56 @@ void launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // row-group partials in the column-partial area of the workspace
         float2* scratch = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                     (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
+        const int nup = nstrip * (diag_ks(nk_tile) == 2 ? dev::diag_up_blocks<2>() : dev::diag_up_blocks<1>());
 #if NTXENT_TIMING
         static TimingBuf tb;
-        q.tstamp = tb.prepare(nstrip * (diag_ks(nk_tile) == 2 ? dev::diag_up_blocks<2>() : dev::diag_up_blocks<1>()), stream);
+        q.tstamp = tb.prepare(nup, stream);
 #endif
-        if (diag_ks(nk_tile) == 2) {
-          const dim3 sg(nstrip * dev::diag_up_blocks<2>());
-          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2>), sg, dim3(256), 0, stream, q, scratch);
-          else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2>), sg, dim3(256), 0, stream, q, scratch);
-        } else {
-          const dim3 sg(nstrip * dev::diag_up_blocks<1>());
-          if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1>), sg, dim3(256), 0, stream, q, scratch);
-          else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1>), sg, dim3(256), 0, stream, q, scratch);
+        auto launch_up = [&](auto side, int nside) {
+          using S = decltype(side);
+          const dim3 sg(nup + nside);
+          if (diag_ks(nk_tile) == 2) {
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2, S>), sg, dim3(256), 0, stream, q, scratch, side);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2, S>), sg, dim3(256), 0, stream, q, scratch, side);
+          } else {
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1, S>), sg, dim3(256), 0, stream, q, scratch, side);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1, S>), sg, dim3(256), 0, stream, q, scratch, side);
+          }
+        };
+        using TS = typename dev::StoreT<Tc>::type;
+        bool side_zt = false;
+        if constexpr (sizeof(TS) == 2) {
+          if (raw && raw->zqt && nup <= ws.num_cus) {
+            // Z^T beside the remainder (the LSE launch then only merges): 2 side blocks per CU next
+            // to its one block per CU (3 blocks of its ~50 KiB LDS fit a CU). Only when the
+            // remainder is at most one block per CU: with more (config 5: 320 blocks) the side
+            // blocks hold the slots its second wave needs (+5 us against the LSE launch's transpose)
+            using Ts = typename std::conditional<std::is_same<Tc, dev::bf16r>::value, __bf16, Tc>::type;
+            NTXENT_CHECK(raw->zt == (std::is_same<TS, __bf16>::value ? DType::BF16 : DType::F16) && g.dim_n % 64 == 0,
+                         "fwd_stats: Z^T dtype must be the plan's backward dtype");
+            dev::DiagSideZt<TS, Ts> zs;
+            zs.nup = nup;
+            zs.h = static_cast<const Ts*>(raw->h);
+            zs.zqt = static_cast<TS*>(raw->zqt);
+            zs.inv = raw->inv;
+            zs.dk = g.dim;
+            zs.ldt = (int)g.ld_t;
+            zs.tx = g.rows_pad / 64;
+            zs.ntiles = zs.tx * (g.dim_n / 64);  // (rows [dim, dim_n) of Z^T: zeros)
+            launch_up(zs, std::min(zs.ntiles, NTXENT_ZT_SIDE_PER_CU * ws.num_cus));
+            side_zt = true;
+          }
         }
+        if (!side_zt) launch_up(dev::NoSide{nup}, 0);
+        zt_done = side_zt;
 #if NTXENT_TIMING
-        tb.dump("diag_up", nstrip * (diag_ks(nk_tile) == 2 ? dev::diag_up_blocks<2>() : dev::diag_up_blocks<1>()), stream);
+        tb.dump("diag_up", nup, stream);
 #endif
       }
     }
   });
   NTXENT_HIP_CHECK(hipGetLastError());
+  return zt_done;
 }
 
 void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void* cbuf,

@@ -1595,8 +1595,20 @@ constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + colu
 // piece merges cost more than the shorter K loop saves: profiles/r5/gemm_timing/diag_up.md)
 template <int KS> constexpr int diag_ksd() { return KS / 2 > 1 ? KS / 2 : 1; }
 template <int KS> constexpr int diag_up_blocks() { return 4 * diag_ksd<KS>() + 6 * KS; }
-template <typename T, int FX, int KS>
-__global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch) {
+// Side job of the launch: blocks [nup, gridDim.x) run side(block, count, smem) instead (the LDS is
+// this kernel's one array). The remainder waits on load latency with one 4-wave block per CU, so a
+// bandwidth-bound job (the raw forward's Z^T, DiagSideZt) runs beside it instead of in a later launch.
+struct NoSide {
+  int nup;
+  __device__ void operator()(int, int, char*) const {}
+};
+template <typename T, int FX, int KS, typename SIDE = NoSide>
+__global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch, const SIDE side) {
+  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
+  if ((int)blockIdx.x >= side.nup) {
+    side((int)blockIdx.x - side.nup, (int)gridDim.x - side.nup, smem);
+    return;
+  }
 #if NTXENT_TIMING
   auto dmark = [&](int k) {
     if (threadIdx.x == 0) p.tstamp[(long long)blockIdx.x * kTimingItems * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
@@ -1609,14 +1621,13 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   typedef typename MM::frag frag;
   typedef typename StoreT<T>::type TS;
   typedef __attribute__((address_space(3))) const frag lds_frag;
-  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   lds_char* lds = (lds_char*)smem;
   // scalar wave index (scalar M0 arithmetic for the DMA pieces, as sim_gemm_kernel: -0.3 us)
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int KSD = diag_ksd<KS>();                  // K pieces of a diagonal region
   constexpr int NB = diag_up_blocks<KS>();            // blocks per tile
-  const int nt_d = gridDim.x / NB;                    // diagonal tiles in this launch
-  const int idx = xcd_remap(blockIdx.x, gridDim.x);  // a tile's blocks share one XCD
+  const int nt_d = side.nup / NB;                    // diagonal tiles in this launch
+  const int idx = xcd_remap(blockIdx.x, side.nup);  // a tile's blocks share one XCD
   const int tile = idx / NB, s = idx % NB;
   const bool dg = s < 4 * KSD;
   const int q = dg ? 0 : (s - 4 * KSD) / KS;                     // off-diagonal pair 0..5

@@ -150,6 +150,8 @@ void Engine::forward(const void* h, hipStream_t s) {
   rr.h = h;
   rr.in = cfg_.input;
   rr.inv = inv_;
+  rr.zqt = zqt_local;
+  rr.zt = bwd_;
   // forward GEMM operand: the e4m3 rows for fp8 plans, else zq itself (or the input rows: raw)
   char* op_all = f8_ ? zq8_all_ : zq_all_;
   const size_t op_bytes = f8_ ? Rp * g_.ld_k8 : Rp * g_.ld_k * cs_;
@@ -184,13 +186,14 @@ void Engine::forward(const void* h, hipStream_t s) {
     zqt_pending_ = true;
   }
   // both forward launches overlap a gather (rows, then ZqT): leave CUs for the RCCL kernels
+  bool zt_fwd = false;  // Z^T written by the forward launch (raw, beside the diagonal remainder)
   GemmWorkspace ws_ovl = ws_;
   if (world_ > 1) ws_ovl.sched_cus = std::max(1, ws_.num_cus - std::min(cfg_.comm_reserve_cus, ws_.num_cus / 2));
   {
     NTXENT_TRACE("ntxent.fwd_gemm.own");
     fault_point("fwd");
-    launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s, BlockView{},
-                     nullptr, own_diag_tail(g_), nullptr, raw ? &rr : nullptr);
+    zt_fwd = launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_, n_own_, part_, sbuf_, ws_ovl, g_, s,
+                              BlockView{}, nullptr, own_diag_tail(g_), nullptr, raw ? &rr : nullptr);
   }
   if (n_fwd_ > n_own_) {
     NTXENT_TRACE("ntxent.fwd_gemm.remote");
@@ -208,8 +211,8 @@ void Engine::forward(const void* h, hipStream_t s) {
       q8.zq8t = zq8t_;
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, zq_local, nullptr, &q8);
     } else if (world_ == 1)
-      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, raw ? nullptr : zq_local, zqt_local,
-                 nullptr, raw ? &rr : nullptr);
+      launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s, bwd_, raw ? nullptr : zq_local,
+                 zt_fwd ? nullptr : zqt_local, nullptr, raw && !zt_fwd ? &rr : nullptr);
     else
       launch_lse(part_, ypos_, lse2_all_, cpos_, block_loss_, loss_, g_, s);
   }

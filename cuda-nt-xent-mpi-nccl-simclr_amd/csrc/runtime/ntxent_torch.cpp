@@ -630,20 +630,22 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
     raw.h = h.data_ptr();
     raw.in = in;
     raw.inv = inv.data_ptr<float>();
+    auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, opts(h, to_scalar(P->bwd())));
+    raw.zqt = zqt.data_ptr();
+    raw.zt = P->bwd();
     auto part = at::empty({P->g.col_tiles, P->g.rows_pad, 2}, opts(h, at::kFloat));
     auto sc = at::empty({(long)P->n_fwd * kTileElems}, opts(h, to_scalar(P->bwd())));
     auto ws = gemm_ws(h, P->n_fwd, *P);
-    launch_fwd_stats(P->comp, nullptr, nullptr, reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd,
+    const bool zt_fwd = launch_fwd_stats(P->comp, nullptr, nullptr, reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd,
                      reinterpret_cast<float2*>(part.data_ptr<float>()), sc.data_ptr(), ws, P->g, s, BlockView{}, nullptr,
                      P->n_fwd == P->n_own ? own_diag_tail(P->g) : 0, nullptr, &raw);
     auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
     auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
-    auto zqt = at::empty({P->g.dim_n, P->g.ld_t}, opts(h, to_scalar(P->bwd())));
     auto block_loss = device_scratch(h, (size_t)lse_scratch_floats(P->g) * 4, 1);
     auto loss = at::empty({}, opts(h, at::kFloat));
     launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(), lse2.data_ptr<float>(),
                cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()), loss.data_ptr<float>(), P->g, s,
-               P->bwd(), nullptr, zqt.data_ptr(), nullptr, &raw);
+               P->bwd(), nullptr, zt_fwd ? nullptr : zqt.data_ptr(), nullptr, zt_fwd ? nullptr : &raw);
     return {loss, at::empty({0}, opts(h, to_scalar(P->bwd()))), zqt, inv, lse2, sc, cpos};
   }
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
