@@ -548,6 +548,8 @@ struct LseArgs {
   // units); null otherwise
   float* mneg2;
   float* lmin;
+  // > 0: the loss sum as one fixed-point ticket (lse_block), 2^F units per nat (lse_loss_fx)
+  double loss_fx;
 };
 // Block `bid` of the nb LSE blocks (the last of them to finish sums the loss).
 __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, float* red, int& last) {
@@ -618,6 +620,28 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
     if (a.mneg2) a.mneg2[own0 + i] = kNegInf;
   }
   const float tot = block_sum(li, red);
+  const bool fx = a.loss_fx > 0.0;
+  if (fx) {
+    // One 64-bit ticket carries the arrival (bits 0-11), a non-finite partial (bits 12-23) and the
+    // partial in fixed point (bits 24-63, loss_fx units: launch_lse sizes it so the whole sum fits
+    // 40 bits). Integer adds commute, so the sum is deterministic whoever arrives last, and the
+    // partial needs no store + drain + reload around the ticket (two memory round trips fewer on
+    // the launch's critical path than the float form below).
+    if (threadIdx.x == 0) {
+      unsigned long long* tk = reinterpret_cast<unsigned long long*>(a.block_loss + 2);
+      const bool fin = tot >= 0.f && tot < 3.0e38f;
+      const unsigned long long q = fin ? (unsigned long long)llrint((double)tot * a.loss_fx) : 0ull;
+      const unsigned long long add = (q << 24) | (fin ? 1ull : (1ull << 12) | 1ull);
+      const unsigned long long old = __hip_atomic_fetch_add(tk, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(old & 0xFFF) == nb - 1) {
+        __hip_atomic_store(tk, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long all = old + add;
+        a.loss_sum[0] = ((all >> 12) & 0xFFF) ? __builtin_nanf("")
+                                               : (float)((double)(all >> 24) / a.loss_fx * (double)a.loss_scale);
+      }
+    }
+    if (!a.lmin) return;  // (fp8 backward: the LSE minimum still takes the partials below)
+  }
   const float bmin = a.lmin ? -block_max(-lmn, red) : 0.f;
   // Last-block-done final sum (replaces a separate one-thread launch): publish this block's
   // partial, count arrivals; the last block adds all partials in block order (deterministic)
@@ -642,7 +666,7 @@ __device__ __forceinline__ void lse_block(const LseArgs& a, int bid, int nb, flo
     for (int b = threadIdx.x; b < nb; b += 64)
       s += __hip_atomic_load(partial + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s = wave_sum(s);  // fixed lane assignment and tree: deterministic
-    if (threadIdx.x == 0) a.loss_sum[0] = s * a.loss_scale;
+    if (threadIdx.x == 0 && !fx) a.loss_sum[0] = s * a.loss_scale;
     if (a.lmin) {
       float m = kPosInf;
       for (int b = threadIdx.x; b < nb; b += 64)
@@ -1509,6 +1533,17 @@ static int lse_blocks(const Geometry& g) { return ((g.rows_pad - g.rows / 2) * d
 
 int lse_scratch_floats(const Geometry& g) { return 64 + 2 * lse_blocks(g); }  // counter slot + partials (sum, min)
 
+// Fixed-point scale of the LSE launch's loss ticket (lse_block): 2^F units per nat with the whole
+// sum below 2^40 units. Every loss term is softplus(lse_neg - y_pos) <= log(2N) + 2 / tau + 1
+// (unit rows: logits within +-1/tau), so F = 39 - ceil(log2(R * that)); 0 (the float partials
+// and their reload) when nb exceeds the ticket's 12-bit arrival count.
+static double lse_loss_fx(const Geometry& g, int nb) {
+  if (nb >= 4095) return 0.0;
+  const double bound = (double)g.rows * (std::log(2.0 * (double)g.global_rows) + 2.0 / g.temperature + 1.0) + 64.0;
+  const int F = 39 - (int)std::ceil(std::log2(bound));
+  return std::ldexp(1.0, F);
+}
+
 void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* cpos, float* block_loss,
                 float* loss_sum, const Geometry& g, hipStream_t stream, DType tr_dtype, const void* zq, void* zqt,
                 const Q8Stats* q8, const RawRows* raw) {
@@ -1519,6 +1554,7 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
     a.mneg2 = q8->mneg2;
     a.lmin = q8->lmin;
   }
+  a.loss_fx = lse_loss_fx(g, nb);
   if (raw) {  // Z^T = (h * inv)^T straight from the input rows (raw-operand forward)
     NTXENT_CHECK(zqt != nullptr && q8 == nullptr && raw->inv && (tr_dtype == DType::F16 || tr_dtype == DType::BF16) &&
                      g.rows == g.rows_pad && g.dim == g.dim_k, "lse (raw rows): 2-byte Z^T, rows % 256 == 0, dim % 64 == 0");
