@@ -726,6 +726,71 @@ __device__ __forceinline__ void dz8_finish(f32x4 (&acc)[8][4], const SimParams& 
   }
 }
 
+// h tile of the fused dZ epilogue prefetched into the ring (dz_store_h): 8 pieces of 128 rows x
+// 128 B (piece i = rows 128 (i & 1).., bytes 128 (i >> 1).. of the tile's 512-byte row segment,
+// the ring's chunk swizzle), DMA'd by the last two K-steps in place of their trailing (clamped)
+// stages: pieces 0-6 into the ring slots those stages would fill, piece 7 into 16 KiB past the
+// per-row coefficients. LDS byte offset of piece i:
+__device__ __forceinline__ constexpr int hpiece_lds(int i) {
+  return i == 0 ? 0 : i == 1 ? kStageBytes : i == 2 ? kStageBytes + kHalfBytes : i == 3 ? kHalfBytes
+       : i == 4 ? kTile * kKStepBytes : i == 5 ? kStageBytes + kTile * kKStepBytes
+       : i == 6 ? kStageBytes + kTile * kKStepBytes + kHalfBytes : kGemmLds + 2048;
+}
+constexpr int kHPieceExtra = 16384;  // piece 7's LDS (dZ kernels of 16-bit plans)
+
+// Fused normalisation backward from the prefetched h tile (hpiece_lds): each lane reads the h
+// values of its own accumulator fragments (8 B = 4 columns of one row, conflict-free: 16 lanes =
+// 16 rows of distinct swizzled granules), writes dh over them in place, and the tile leaves as
+// 128-byte row segments. No fp16 staging of g and no h loads after the main loop, where they
+// waited on memory with the whole chip at once (dz_store below).
+__device__ __forceinline__ void dz_store_h(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
+                                           const int (&rb)[8], const int (&cb)[4], lds_char* lds, float iv0, float dt0) {
+  typedef __attribute__((address_space(3))) u32x2 lds_u2;
+  typedef __attribute__((address_space(3))) u32x4 lds_u4;
+  typedef __attribute__((address_space(3))) f32x2 lds_f2;
+  const int lane = tid & 63, wb = (tid >> 6) & 3;
+  const float sgo = p.ngo[0] * p.nalpha;
+  lds_f2* cf = (lds_f2*)(lds + kTile * 512);  // [256] per-row (c1, c2)
+  if (tid < kTile) cf[tid] = f32x2{sgo * iv0, sgo * iv0 * iv0 * dt0};
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's h pieces landed
+  __syncthreads();                                   // everyone's, and the coefficients
+  const bool bf = p.nh_dt == 2;
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int r = (rb[mi] & 127) + (lane & 15);  // row inside piece half mi >> 2
+    const f32x2 c = cf[rb[mi] + (lane & 15)];
+    const int rofs = r * kKStepBytes;
+    const int sw = (r >> 1) & 7;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int nn = (cb[ni] + 4 * (lane >> 4)) & 63;  // column inside the piece's 64
+      // piece 2 cq + rh: cq = 2 (ni >> 1) + (wb >> 1) (wave-uniform), rh = mi >> 2
+      const int a = (wb >> 1) ? hpiece_lds(4 * (ni >> 1) + 2 + (mi >> 2)) : hpiece_lds(4 * (ni >> 1) + (mi >> 2));
+      lds_u2* hp = (lds_u2*)(lds + a + rofs + (((nn >> 3) ^ sw) << 4) + ((nn & 7) << 1));
+      union { _Float16 f[4]; __bf16 b[4]; u32x2 u; } x, y;
+      x.u = *hp;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = (float)(_Float16)acc[mi][ni][e];
+        const float hv = bf ? (float)x.b[e] : (float)x.f[e];
+        const float o = c.x * g - c.y * hv;
+        if (bf) y.b[e] = (__bf16)o;
+        else y.f[e] = (_Float16)o;
+      }
+      *hp = y.u;
+    }
+  }
+  __syncthreads();
+  const long long nd = p.nd;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int i = k >> 1, r = (tid >> 3) + 64 * (k & 1), c = tid & 7;
+    const u32x4 v = *(lds_u4*)(lds + hpiece_lds(i) + r * kKStepBytes + ((c ^ ((r >> 1) & 7)) << 4));
+    const long long m = (long long)mt * kTile + 128 * (i & 1) + r;
+    store16_wt(p.ndh, (m * nd + nt * kTile + 64 * (i >> 1) + 8 * c) * 2, v);
+  }
+}
+
 // dZ epilogue (swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r])
 // of output tile (mt, nt); `lds` (>= 128 KiB, free) stages the fp16 tile for coalesced rows.
 __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
@@ -877,7 +942,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // forward: + 12 KiB of row / column reductions, + 4 KiB: the raw-operand ring of row inverse
   // norms (2 slots x [256 A rows | 256 B rows], filled by 4-byte LDS-DMA one item ahead)
   constexpr int kInvLds = kFwdRed + (MODE == kModeFwd ? 6 * 256 * 8 : 0);
-  __shared__ __attribute__((aligned(16))) char smem[kInvLds + (MODE == kModeFwd && !std::is_same<T, fp8e4m3>::value ? 4096 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[kInvLds + (MODE == kModeFwd && !std::is_same<T, fp8e4m3>::value ? 4096 : 0) +
+                                                     (MODE == kModeDz && !std::is_same<T, fp8e4m3>::value ? kHPieceExtra : 0)];
   lds_char* lds = (lds_char*)smem;
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
 
@@ -919,6 +985,23 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
                                                (unsigned)((128 * h + 16 * w + 8 * j) * (isB ? p.B.ld : p.A.ld)), 0,
                                                kGemmDmaAux);
     s.advance(isB ? p.B : p.A);
+  };
+  // dZ (hpre below): piece i of the epilogue's h tile (hpiece_lds) for output tile (mt_, nt_):
+  // tile rows 128 (i & 1) + 16 w + 8 j + (lane >> 3), bytes 128 (i >> 1) + the ring's swizzled
+  // 16-B chunk of their 512-byte segment, into this wave's 16 rows of the piece's LDS
+  auto stage_h = [&](int i, int mt_, int nt_) {
+    const long long hld = (long long)p.nd * 2;
+    const char* hb = static_cast<const char*>(p.nh) + ((long long)mt_ * kTile + 128 * (i & 1)) * hld +
+                     (long long)nt_ * kTile * 2 + 128 * (i >> 1);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(hb), 0, 0x7FFFFFFF, 0x00020000);
+    lds_char* dst = lds + hpiece_lds(i) + 16 * w * kKStepBytes;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rl = 8 * j + (lane >> 3);
+      const unsigned vo = (unsigned)((lane >> 3) * hld) + (unsigned)((((lane & 7) ^ ((rl >> 1) & 7))) << 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + 8 * j * kKStepBytes), 16, vo,
+                                               (unsigned)((16 * w + 8 * j) * hld), 0, kGemmDmaAux);
+    }
   };
 
   f32x4 acc[8][4];
@@ -1190,8 +1273,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // K-steps in pairs: the buffer parity is a compile-time constant in each copy, so the LDS
   // read addresses are loop-invariant registers + immediates (headline dZ -1.9 %, forward -1.5 %,
   // config 5 dZ -3.4 %: profiles/r4/variants_r4_v21_unroll2.md)
-  auto kstep = [&](const int ks, auto cur_c) {
+  // dZ with the fused normalisation backward of 16-bit rows on a whole tile: the last two K-steps
+  // (TAIL 1, 2) stage the epilogue's h tile (dz_store_h) instead of their trailing clamped stages
+  bool hpre = false;
+  if constexpr (MODE == kModeDz && !kF8)
+    hpre = p.ndh != nullptr && (p.nh_dt == 1 || p.nh_dt == 2) && stile < 0 && nsteps == nk && nsteps >= 4 &&
+           (nsteps & 1) == 0 && p.R % kTile == 0 && p.nd % kTile == 0;
+  auto kstep = [&](const int ks, auto cur_c, auto tail_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
+    constexpr int TAIL = decltype(tail_c)::value;
     if constexpr (kStreamMode) {
       // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
       if (cont && ks == nsteps - 2) {
@@ -1206,33 +1296,61 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     read_a(cur, 0, af);             //   operand reads first: their latency hides under the
     __builtin_amdgcn_sched_barrier(0);  // pin: the 8 A0 reads precede the B0 reads (a0_retire)
     read_b(cur, 0, bf0);            //   DMA issue that follows (~100-200 cycles per piece)
-    stage(0, 1, sa1, nxt);          //   A1 of step ks+1
+    if constexpr (TAIL == 2) stage_h(3, mt, nt);
+    else stage(0, 1, sa1, nxt);     //   A1 of step ks+1
     a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
     lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
     mma_quadrant(kI0, kI0, af, bf0);
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
     read_b(cur, 1, bf1);
-    stage(0, 0, sa0, cur);          //   A0 of step ks+2
+    if constexpr (TAIL != 0) stage_h(TAIL == 1 ? 0 : 4, mt, nt);
+    else stage(0, 0, sa0, cur);     //   A0 of step ks+2
     barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
     mma_quadrant(kI0, kI1, af, bf1);
     barrier();                      // phase 3 L
     read_a(cur, 1, af);
-    stage(1, 0, sb0, cur);          //   B0 of step ks+2
+    if constexpr (TAIL != 0) stage_h(TAIL == 1 ? 1 : 5, mt, nt);
+    else stage(1, 0, sb0, cur);     //   B0 of step ks+2
     barrier(); lds_drain();         // phase 3 C (A1 is restaged two phases later)
     mma_quadrant(kI1, kI0, af, bf0);
-    dma_wait(); barrier();          // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1)
-    stage(1, 1, sb1, cur);          //   B1 of step ks+2
+    // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1; the last K-step of an h-prefetch
+    // tail has none, and its wait would be the first to hold for the h pieces' memory latency)
+    if constexpr (TAIL != 2) dma_wait();
+    barrier();
+    if constexpr (TAIL != 0) {
+      stage_h(TAIL == 1 ? 2 : 6, mt, nt);
+      if constexpr (TAIL == 2) stage_h(7, mt, nt);  // (its own LDS: no wait counted after it)
+    } else {
+      stage(1, 1, sb1, cur);        //   B1 of step ks+2
+    }
     barrier();                      // phase 4 C
     mma_quadrant(kI1, kI1, af, bf1);
   };
+  const std::integral_constant<int, 2> kI2{};
   int ks2 = 0;
-  for (; ks2 + 1 < nsteps; ks2 += 2) {
-    kstep(ks2, kI0);
-    kstep(ks2 + 1, kI1);
+  const int nmain = nsteps - (hpre ? 2 : 0);
+  for (; ks2 + 1 < nmain; ks2 += 2) {
+    kstep(ks2, kI0, kI0);
+    kstep(ks2 + 1, kI1, kI0);
   }
-  if (ks2 < nsteps) kstep(ks2, kI0);
+  if constexpr (MODE == kModeDz && !kF8) {
+    if (hpre) {
+      kstep(ks2, kI0, kI1);
+      kstep(ks2 + 1, kI1, kI2);
+      ks2 += 2;
+    }
+  }
+  if (ks2 < nsteps) kstep(ks2, kI0, kI0);
   if (grp == 0) barrier();  // re-align the groups
   tmark(item, 2);
+  // dZ, h prefetched: this thread's row statistics for the epilogue, loaded before the drain
+  float hiv = 0.f, hdt = 0.f;
+  if constexpr (MODE == kModeDz && !kF8) {
+    if (hpre && threadIdx.x < kTile) {
+      hiv = p.ninv[mt * kTile + threadIdx.x];
+      hdt = p.ndot[mt * kTile + threadIdx.x];
+    }
+  }
   if (kStreamMode && cont) {
     // the trailing stages are the next item's K-steps 0 and 1 (buffers of parity nk): leave
     // them in flight; this epilogue's stores will be younger than them
@@ -1289,7 +1407,8 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   if constexpr (MODE == kModeDz) {
     if constexpr (kF8) dz8_finish(acc, p, mt, nt, rb, cb, lane);
-    dz_store(acc, p, mt, nt, tid, rb, cb, lds);
+    if (!kF8 && hpre) dz_store_h(acc, p, mt, nt, tid, rb, cb, lds, hiv, hdt);
+    else dz_store(acc, p, mt, nt, tid, rb, cb, lds);
   } else if constexpr (MODE == kModeCoef) {
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
