@@ -64,6 +64,13 @@ def parse(argv=None):
                     help="N>1: symmetric = each rank pair's similarity block computed once (column partials and "
                          "partner gradient contributions exchanged point to point); allgather = every rank computes "
                          "its whole row block against the gathered rows; ring = O(local) memory")
+    ap.add_argument("--dist-impl", default="auto", choices=["auto", "engine", "torch"],
+                    help="N>1, --impl fused: auto/engine = the native C++ engine behind autograd "
+                         "(parallel/engine_loss.py: one C++ call per forward/backward, its own RCCL "
+                         "communicator); torch = the Python-driven stages over torch.distributed")
+    ap.add_argument("--host-profile", default=None,
+                    help="rank 0: cProfile of 10 extra steps' host enqueue after the timed region, top "
+                         "entries written to this path (where the host time of a step goes)")
     ap.add_argument("--data", default="views", choices=["views", "iid"],
                     help="views: two noisy views of a shared random-normal basis (positives correlated, "
                          "as from a SimCLR encoder); iid: independent random-normal rows")
@@ -276,7 +283,7 @@ def run_rank(a) -> None:
                 loss = torch_ntxent(h, a.temperature)
             elif world > 1:
                 loss = dist_ntxent_loss(h, a.temperature, compute=compute, keep_logits=not a.recompute,
-                                        overlap=not a.no_overlap, negatives=a.negatives)
+                                        overlap=not a.no_overlap, negatives=a.negatives, impl=a.dist_impl)
             else:
                 loss = ntxent_amd.ntxent_loss(h, a.temperature, compute=compute, keep_logits=not a.recompute)
             (gh,) = torch.autograd.grad(loss, h, grad_outputs=one.to(loss.dtype))
@@ -359,9 +366,20 @@ def run_rank(a) -> None:
     per_ms = comm_ms = None
     if on_gpu or world > 1:
         _, per_ms, comm_ms, _, _ = timed(step, min(a.steps, 20), 1, per_step_events=on_gpu, comm=world > 1)
-    # torch allocator peak, plus the native Engine's own arena (allocated once, outside torch)
-    peak_mb = ((torch.cuda.max_memory_allocated(dev) + getattr(make_step, "engine_bytes", 0)) / 2**20
-               if on_gpu else None)
+    if a.host_profile and rank == 0:
+        host_profile(step, a.host_profile, sync)
+    elif a.host_profile:
+        for _ in range(10):  # the same steps as rank 0 (they run collectives)
+            step()
+        sync()
+    # torch allocator peak, plus the native Engine arenas (allocated once, outside torch)
+    from ntxent_amd.parallel.engine_loss import cached_engine_bytes
+
+    dist_impl = None
+    if world > 1 and a.impl == "fused":
+        dist_impl = "engine" if cached_engine_bytes() > 0 else "torch"
+    peak_mb = ((torch.cuda.max_memory_allocated(dev) + getattr(make_step, "engine_bytes", 0)
+                + cached_engine_bytes()) / 2**20 if on_gpu else None)
     lossv = float(loss.item())
     finite = bool(lossv == lossv and torch.isfinite(gh).all().item())
 
@@ -408,7 +426,7 @@ def run_rank(a) -> None:
     if rank == 0:
         if not ok:
             raise SystemExit("non-finite loss or gradient")
-        mfma = a.compute if a.compute != "auto" else ("fp32" if a.dtype == "fp32" else "fp16")
+        mfma = mfma_dtypes(a, world, rank, dev) if on_gpu else {"forward": None, "backward": None}
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -435,10 +453,12 @@ def run_rank(a) -> None:
                 "dim": a.dim,
                 "temperature": a.temperature,
                 "compute": a.compute,
-                "mfma_dtype": mfma,
+                "mfma_dtype_forward": mfma["forward"],
+                "mfma_dtype_backward": mfma["backward"],
                 "keep_logits": not a.recompute,
                 "parallelism": f"dp{world}",
                 "negatives": a.negatives if world > 1 else None,
+                "dist_impl": dist_impl,
                 "backend": backend if world > 1 else None,
                 "hip_graph": bool(a.graph),
                 "compute_stream": a.compute_stream if on_gpu else None,
@@ -474,7 +494,62 @@ def run_rank(a) -> None:
             Path(a.json_out).write_text(line + "\n")
     if world > 1:
         dist.barrier()
+        from ntxent_amd.parallel.engine_loss import release_engines
+
+        release_engines()
         dist.destroy_process_group()
+
+
+def mfma_dtypes(a, world: int, rank: int, dev) -> dict:
+    """The MFMA operand dtypes the forward and backward GEMMs of this configuration run."""
+    from ntxent_amd.ops import _ext
+    from ntxent_amd.ops.ntxent import resolve_compute
+
+    dt_in = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[a.dtype]
+    comp = resolve_compute(dt_in, False, a.compute)
+    if a.impl == "torch":
+        return {"forward": "hipBLASLt " + a.dtype, "backward": "hipBLASLt " + a.dtype}
+    C = _ext.load()
+    R = 2 * a.batch
+    plan = C.get_plan(R, a.dim, world, rank, float(a.temperature), comp, dev.index)
+    name = {"fp32": "fp32 (v_mfma_f32_16x16x4_f32)", "fp16": "fp16 (v_mfma_f32_16x16x32_f16)",
+            "bf16": "bf16 (v_mfma_f32_16x16x32_bf16)", "fp8": "e4m3 (block-scaled v_mfma_scale_f32_*_f8f6f4)"}
+    if plan.small:
+        fwd = plan.compute_dtype
+    elif comp == "fp8":
+        fwd = "fp8"
+    elif (world == 1 and not a.recompute and C.raw_forward_enabled() and a.dtype in ("bf16", "fp16")
+          and comp in ("fp16", a.dtype) and R % 256 == 0 and a.dim % 64 == 0):
+        fwd = a.dtype  # raw-operand forward: the input rows themselves are the MFMA operands
+    else:
+        fwd = plan.compute_dtype
+    bwd = ("fp8" if comp == "fp8" and world == 1 and C.fp8_backward_enabled() and a.dim % 8 == 0 and not plan.small
+           else plan.backward_dtype)
+    return {"forward": name.get(fwd, fwd), "backward": name.get(bwd, bwd)}
+
+
+def host_profile(step, path: str, sync) -> None:
+    """cProfile of the host side of 10 steps (the GPU runs behind); top entries by own time."""
+    import cProfile
+    import io
+    import pstats
+
+    sync()
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    for _ in range(10):
+        step()
+    pr.disable()
+    t_enq = (time.perf_counter() - t0) / 10 * 1e3
+    sync()
+    buf = io.StringIO()
+    st = pstats.Stats(pr, stream=buf)
+    st.sort_stats("tottime").print_stats(40)
+    buf2 = io.StringIO()
+    pstats.Stats(pr, stream=buf2).sort_stats("cumulative").print_stats(40)
+    Path(path).write_text(f"host enqueue under cProfile: {t_enq:.3f} ms/step (10 steps; profiling adds overhead)\n\n"
+                          f"== by own time ==\n{buf.getvalue()}\n== by cumulative time ==\n{buf2.getvalue()}")
 
 
 def main(argv=None):

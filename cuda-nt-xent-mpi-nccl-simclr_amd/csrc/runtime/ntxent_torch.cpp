@@ -919,12 +919,17 @@ class NativeEngine {
  public:
   NativeEngine(int rows, int dim, double T, const std::string& input, const std::string& compute,
                const std::string& negatives, int rank, int world, const std::string& uid, int device, bool keep_cos,
-               int comm_reserve_cus)
+               int comm_reserve_cus, std::shared_ptr<RcclComm> comm = nullptr)
       : device_(device) {
     NTXENT_CHECK(world >= 1 && rank >= 0 && rank < world, "NativeEngine: bad rank/world");
     NTXENT_CHECK(negatives == "symmetric" || negatives == "allgather", "negatives must be symmetric|allgather");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(device);
-    if (world > 1) comm_ = std::make_unique<RcclComm>(rank, world, uid, device);
+    if (comm) {  // a communicator shared by every engine of this process group (one RCCL init)
+      NTXENT_CHECK(comm->rank() == rank && comm->world() == world, "NativeEngine: communicator rank/world mismatch");
+      comm_ = std::move(comm);
+    } else if (world > 1) {
+      comm_ = std::make_shared<RcclComm>(rank, world, uid, device);
+    }
     EngineConfig cfg;
     cfg.rows = rows;
     cfg.dim = dim;
@@ -1010,7 +1015,7 @@ class NativeEngine {
   }
   int device_ = 0;
   at::ScalarType in_ = at::kBFloat16;
-  std::unique_ptr<RcclComm> comm_;  // declared before eng_: destroyed after it
+  std::shared_ptr<RcclComm> comm_;  // declared before eng_: destroyed after it
   std::unique_ptr<Engine> eng_;
   at::Tensor h_;         // input of the last forward (read by backward)
   at::Tensor gh_, gdh_;  // the captured graph's input and output (alive while the graph exists)
@@ -1069,13 +1074,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readonly("small", &Plan::small)
       .def_readonly("fwd_tiles", &Plan::fwd_tiles)
       .def_readonly("dz_tiles", &Plan::dz_tiles);
+  // one RCCL communicator per (process group, device), shared by the engines of every shape
+  py::class_<ntxent::RcclComm, std::shared_ptr<ntxent::RcclComm>>(m, "RcclCommunicator")
+      .def(py::init([](int rank, int world, const py::bytes& uid, int device) {
+             return std::make_shared<ntxent::RcclComm>(rank, world, std::string(uid), device);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def_property_readonly("rank", &ntxent::RcclComm::rank)
+      .def_property_readonly("world", &ntxent::RcclComm::world)
+      .def("check", &ntxent::RcclComm::check)
+      .def("abort", &ntxent::RcclComm::abort);
   py::class_<NativeEngine>(m, "NativeEngine")
       .def(py::init<int, int, double, const std::string&, const std::string&, const std::string&, int, int,
-                    const std::string&, int, bool, int>(),
+                    const std::string&, int, bool, int, std::shared_ptr<ntxent::RcclComm>>(),
            py::arg("rows"), py::arg("dim"), py::arg("temperature"), py::arg("input") = "bf16",
            py::arg("compute") = "auto", py::arg("negatives") = "symmetric", py::arg("rank") = 0, py::arg("world") = 1,
            py::arg("uid") = std::string(), py::arg("device") = 0, py::arg("keep_cos") = true,
-           py::arg("comm_reserve_cus") = 8)
+           py::arg("comm_reserve_cus") = 8, py::arg("comm") = py::none())
       .def("forward", &NativeEngine::forward, py::arg("h"))
       .def("backward", &NativeEngine::backward, py::arg("grad_out") = py::none())
       .def("loss_tensor", &NativeEngine::loss_tensor)

@@ -188,7 +188,8 @@ def _reduce_scatter_backward(plan, h, zq, zqt_all, inv, lse2_all, grad_out, grou
 
 def dist_ntxent_loss(h_local: torch.Tensor, temperature: float = 0.07, *, group=None, compute: str = "auto",
                      use_mixed_precision: bool = False, keep_logits: bool = True, overlap: bool = True,
-                     backward_mode: str = "symmetric", negatives: str = "allgather") -> torch.Tensor:
+                     backward_mode: str = "symmetric", negatives: str = "allgather",
+                     impl: str = "auto") -> torch.Tensor:
     """Global NT-Xent over the data-parallel group; ``h_local = [h1_r; h2_r]`` on each rank.
 
     backward_mode: ``"symmetric"`` (default: rank-local C = P + P^T - 2 I_pos from the gathered
@@ -199,9 +200,26 @@ def dist_ntxent_loss(h_local: torch.Tensor, temperature: float = 0.07, *, group=
     partials and partner gradient contributions exchanged point to point, see
     :mod:`parallel.symmetric`), or ``"ring"`` (rows passed point-to-point around the ring,
     O(local) memory, see :mod:`parallel.ring`).
+    impl: ``"auto"`` (default: the native C++ engine of :mod:`parallel.engine_loss` whenever it
+    can run the call -- RCCL group, GPU tensors, symmetric or all-gather negatives, symmetric
+    backward, overlap on -- else the torch-driven stages), ``"engine"`` (required; raises if not
+    eligible) or ``"torch"`` (the Python-driven stages over ``torch.distributed``).
     """
     if negatives not in ("allgather", "ring", "symmetric"):
         raise ValueError("negatives must be 'allgather', 'symmetric' or 'ring'")
+    if impl not in ("auto", "engine", "torch"):
+        raise ValueError("impl must be 'auto', 'engine' or 'torch'")
+    if impl != "torch":
+        from .engine_loss import engine_eligible, engine_ntxent_loss
+
+        ok, why = engine_eligible(h_local, group, negatives, backward_mode, overlap)
+        if ok:
+            comp = resolve_compute(h_local.dtype, use_mixed_precision, compute)
+            return engine_ntxent_loss(h_local, temperature, group=group, compute=comp, negatives=negatives,
+                                      keep_logits=keep_logits or negatives == "symmetric",
+                                      comm_reserve_cus=comm_reserve_cus(dist.get_backend(group)))
+        if impl == "engine":
+            raise ValueError(f"dist_ntxent_loss(impl='engine'): not eligible ({why})")
     if negatives == "symmetric":
         from .symmetric import sym_ntxent_loss
 

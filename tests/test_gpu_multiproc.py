@@ -33,7 +33,8 @@ def _shards(W, n, dim, seed):
     return out
 
 
-def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives="allgather", backend="gloo"):
+def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives="allgather", backend="gloo",
+            impl="auto"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -50,10 +51,16 @@ def _worker(rank, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives
         from ntxent_amd.parallel import dist_ntxent_loss
 
         h = _shards(W, n, dim, seed=11)[rank].float().cuda().requires_grad_(True)
+        from ntxent_amd.parallel.engine_loss import cached_engine_bytes, release_engines
+
         loss = dist_ntxent_loss(h, T, compute=compute, keep_logits=keep, overlap=overlap, backward_mode=mode,
-                                negatives=negatives)
+                                negatives=negatives, impl=impl)
         (g,) = torch.autograd.grad(loss, h, torch.tensor(0.7, device=h.device))
         torch.cuda.synchronize()
+        used = "engine" if cached_engine_bytes() > 0 else "torch"
+        release_engines()
+        if impl != "auto" and used != impl:
+            raise RuntimeError(f"asked impl={impl}, ran {used}")
         q.put((rank, loss.item(), g.double().cpu().numpy()))  # by value: no shared-memory fd hand-off
     except Exception as e:  # surface the failure in the parent
         q.put((rank, repr(e), None))
@@ -83,29 +90,68 @@ def test_multiprocess_matches_oracle(W, n, dim, compute, keep, overlap, mode, ne
 # grouped batch_isend_irecv of the symmetric mode, the async all-gathers / reduce-scatter of the
 # all-gather mode and the ring's exchanges run through RCCL's communicator and kernels, with the
 # GEMMs' comm CU reserve active (only the wire is not xGMI).
-@pytest.mark.parametrize("W,n,dim,compute,keep,overlap,mode,negatives", [
-    (2, 512, 128, "fp16", False, True, "symmetric", "symmetric"),
-    (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric"),
-    (3, 384, 80, "fp32", True, True, "symmetric", "symmetric"),
-    (2, 300, 96, "fp16", False, True, "symmetric", "allgather"),
-    (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather"),
-    (2, 256, 128, "fp16", False, True, "symmetric", "ring"),
+# impl: "engine" = the native C++ engine behind autograd (parallel/engine_loss.py, the default of
+# dist_ntxent_loss on RCCL); "torch" = the Python-driven stages over torch.distributed.
+@pytest.mark.parametrize("W,n,dim,compute,keep,overlap,mode,negatives,impl", [
+    (2, 512, 128, "fp16", False, True, "symmetric", "symmetric", "engine"),
+    (2, 512, 128, "fp16", False, True, "symmetric", "symmetric", "torch"),
+    (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric", "engine"),
+    (2, 2048, 64, "fp16", True, True, "symmetric", "symmetric", "torch"),
+    (3, 384, 80, "fp32", True, True, "symmetric", "symmetric", "engine"),
+    (3, 384, 80, "fp32", True, True, "symmetric", "symmetric", "torch"),
+    (2, 300, 96, "fp16", False, True, "symmetric", "allgather", "engine"),
+    (2, 300, 96, "fp16", False, True, "symmetric", "allgather", "torch"),
+    (2, 256, 64, "fp8", True, True, "symmetric", "symmetric", "engine"),
+    (2, 128, 64, "fp32", True, True, "reduce_scatter", "allgather", "torch"),
+    (2, 256, 128, "fp16", False, True, "symmetric", "ring", "torch"),
     # W = 8, the driver's scaling-run world size: 3 full partner blocks + a split pair per rank
     # (symmetric), 7 gathered blocks (all-gather); 8 processes sharing the GPU over sockets
-    (8, 256, 64, "fp16", True, True, "symmetric", "symmetric"),
-    (8, 256, 64, "fp16", False, True, "symmetric", "allgather"),
+    (8, 256, 64, "fp16", True, True, "symmetric", "symmetric", "engine"),
+    (8, 256, 64, "fp16", True, True, "symmetric", "symmetric", "torch"),
+    (8, 256, 64, "fp16", False, True, "symmetric", "allgather", "engine"),
+    (8, 256, 64, "fp16", False, True, "symmetric", "allgather", "torch"),
 ])
-def test_multiprocess_rccl_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives):
-    _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "nccl")
+def test_multiprocess_rccl_matches_oracle(W, n, dim, compute, keep, overlap, mode, negatives, impl):
+    _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, "nccl", impl)
 
 
-def _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, backend):
+def test_config3_shape_rccl_w4(tmp_path):
+    """The SCALE run's per-rank shape (B = 4096 pairs/rank, d = 2048, bf16 inputs: 8192 rows x
+    2048, 32 row tiles, 4 exchange chunks of 8 row tiles per peer, a split pair) at W = 4 over
+    RCCL, both negatives modes on both implementations (tools/w8_full_check.py): symmetric ==
+    all-gather loss, every gradient within 4e-3 of max|g| of an fp32 torch oracle of the global
+    problem, and a per-rank HBM bound (torch allocator peak + the engine arena)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    out = tmp_path / "c3.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        str(root / "tools" / "w8_full_check.py"), "--batch", "4096", "--dim", "2048", "--steps", "1",
+                        "--grad-tol", "4e-3", "--impls", "engine,torch", "--json-out", str(out)],
+                       capture_output=True, text=True, timeout=280, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = json.loads(out.read_text())
+    assert d["ok"] and d["world"] == 4 and d["runs"] == ["symmetric/engine", "allgather/engine",
+                                                          "symmetric/torch", "allgather/torch"]
+    for p in d["per_rank"]:
+        assert p["loss_rel_sym_vs_ag"] <= 1e-6, p
+        assert p["grad_err_sym_vs_fp32"] <= 4e-3 and p["grad_err_ag_vs_fp32"] <= 4e-3, p
+        assert 0 < p["peak_mib_symmetric"] <= 3072 and 0 < p["peak_mib_allgather"] <= 3072, p
+    assert d["loss_rel_err_vs_fp32"] <= 1e-5
+
+
+def _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, backend, impl="auto"):
     T = 0.1
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, W, port, n, dim, T, compute, keep, overlap, mode, q, negatives,
-                                               backend))
+                                               backend, impl))
              for r in range(W)]
     for p in procs:
         p.start()
@@ -121,7 +167,7 @@ def _run_and_check(W, n, dim, compute, keep, overlap, mode, negatives, backend):
     hg = R.global_pair_order([s.float().double() for s in _shards(W, n, dim, seed=11)]).requires_grad_(True)
     lref = R.ntxent_loss(hg, T)
     (gref,) = torch.autograd.grad(lref, hg, torch.tensor(0.7, dtype=torch.float64))
-    lt, gt = {"fp32": (2e-5, 2e-4), "fp16": (3e-3, 2e-2)}[compute]
+    lt, gt = {"fp32": (2e-5, 2e-4), "fp16": (3e-3, 2e-2), "fp8": (5e-2, 0.3)}[compute]  # fp8: e4m3 rows vs the unquantised oracle
     scale = gref.abs().max().item()
     N = W * n
     for r in range(W):

@@ -11,7 +11,8 @@ Every rank holds B pairs (2B rows, d) of synthetic two-view data, as ``bench.py`
 Checks, at the shape the driver's 8-GPU SCALE run uses (B = 4096/rank, d = 2048, W = 8):
 
 * the symmetric (``negatives="symmetric"``) and all-gather losses agree, and each rank's
-  gradient from the two modes agrees to fp16-operand tolerance;
+  gradient from the two modes agrees to fp16-operand tolerance, for each ``--impls`` entry
+  (the native engine behind autograd, the default on RCCL, and the torch-driven stages);
 * both agree with an fp32 torch computation of the global problem (torch ops only, sharded
   like the all-gather path: each rank's rows against the gathered fp32 rows);
 * peak HBM per rank of each mode (``torch.cuda.max_memory_allocated`` around one step).
@@ -46,6 +47,9 @@ def main():
     ap.add_argument("--oracle", default="fp32", choices=["fp32", "none"])
     ap.add_argument("--loss-tol", type=float, default=2e-4, help="relative loss tolerance")
     ap.add_argument("--grad-tol", type=float, default=2e-2, help="max|dg| / max|g| tolerance")
+    ap.add_argument("--impls", default="engine,torch",
+                    help="dist_ntxent_loss implementations to check (engine: the native C++ engine "
+                         "behind autograd, the default on RCCL; torch: the Python-driven stages)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo + the torch CPU paths (plumbing test of this script)")
@@ -81,28 +85,37 @@ def main():
     del base, v1, v2
     one = torch.ones((), device=dev)
 
+    from ntxent_amd.parallel.engine_loss import cached_engine_bytes, release_engines
+
+    impls = [i for i in a.impls.split(",") if i] if on_gpu else ["torch"]
+    runs = [(m, i) for i in impls for m in ("symmetric", "allgather")]
     res = {}
-    for mode in ("symmetric", "allgather"):
+    for mode, impl in runs:
         sync()
         dist.barrier()
         if on_gpu:
             torch.cuda.reset_peak_memory_stats(dev)
         base_mb = torch.cuda.memory_allocated(dev) / 2**20 if on_gpu else 0.0
+        arena0 = cached_engine_bytes()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            loss = dist_ntxent_loss(h, a.temperature, negatives=mode)
+            loss = dist_ntxent_loss(h, a.temperature, negatives=mode, impl=impl)
             (gh,) = torch.autograd.grad(loss, h, grad_outputs=one)
         sync()
         dt = (time.perf_counter() - t0) / a.steps
-        peak = torch.cuda.max_memory_allocated(dev) / 2**20 - base_mb if on_gpu else 0.0
-        res[mode] = (float(loss.item()), gh.detach().float(), peak, dt * 1e3)
+        # torch allocator peak of the step + the engine arena this mode created (outside torch)
+        peak = (torch.cuda.max_memory_allocated(dev) / 2**20 - base_mb + (cached_engine_bytes() - arena0) / 2**20
+                if on_gpu else 0.0)
+        res[(mode, impl)] = (float(loss.item()), gh.detach().float(), peak, dt * 1e3)
         del gh, loss
+    release_engines()
 
-    ls, gs, peak_s, ms_s = res["symmetric"]
-    la, ga, peak_a, ms_a = res["allgather"]
+    # every run against the first all-gather run (loss, gradient), and the first two as before
+    ls, gs, peak_s, ms_s = res[runs[0]]
+    la, ga, peak_a, ms_a = res[runs[1]]
     gmax = ga.abs().max().item()
-    err_sa = (gs - ga).abs().max().item() / max(gmax, 1e-30)
-    loss_sa = abs(ls - la) / max(abs(la), 1e-30)
+    err_sa = max((res[k][1] - ga).abs().max().item() for k in runs) / max(gmax, 1e-30)
+    loss_sa = max(abs(res[k][0] - la) for k in runs) / max(abs(la), 1e-30)
 
     # fp32 torch oracle of the global problem, sharded the all-gather way (each rank: its rows
     # against the gathered fp32 rows; ops/reference.sharded_forward_backward, which the CPU
@@ -145,12 +158,16 @@ def main():
             mine = inv.unsqueeze(1) * (dz - z * dot)
             del dz, z
         gm = mine.abs().max().item()
-        err_ref = [(gs - mine).abs().max().item() / gm, (ga - mine).abs().max().item() / gm]
+        err_runs = [(res[k][1] - mine).abs().max().item() / gm for k in runs]
+        err_ref = [max(e for k, e in zip(runs, err_runs) if k[0] == "symmetric"),
+                   max(e for k, e in zip(runs, err_runs) if k[0] == "allgather")]
         del mine
 
-    row = torch.tensor([loss_sa, err_sa, peak_s, peak_a, ms_s, ms_a,
+    row = torch.tensor([loss_sa, err_sa, max(res[k][2] for k in runs if k[0] == "symmetric"),
+                        max(res[k][2] for k in runs if k[0] == "allgather"), ms_s, ms_a,
                         -1.0 if err_ref[0] is None else err_ref[0],
-                        -1.0 if err_ref[1] is None else err_ref[1]], dtype=torch.float64, device=dev)
+                        -1.0 if err_ref[1] is None else err_ref[1]]
+                       + [res[k][2] for k in runs] + [res[k][0] for k in runs], dtype=torch.float64, device=dev)
     allrows = [torch.empty_like(row) for _ in range(world)]
     dist.all_gather(allrows, row)
     ok = True
@@ -158,12 +175,16 @@ def main():
         per = [r.tolist() for r in allrows]
         worst_grad = max(max(p[1], p[6], p[7]) for p in per)
         worst_loss = max(p[0] for p in per)
-        lref_err = None if loss_ref is None else max(abs(ls - loss_ref), abs(la - loss_ref)) / abs(loss_ref)
+        nr = len(runs)
+        losses = {f"{m}/{i}": per[0][8 + nr + j] for j, (m, i) in enumerate(runs)}
+        lref_err = None if loss_ref is None else max(abs(v - loss_ref) for v in losses.values()) / abs(loss_ref)
         ok = worst_grad <= a.grad_tol and worst_loss <= a.loss_tol and (lref_err is None or lref_err <= a.loss_tol)
         out = {
             "check": "w8_full", "ok": ok, "world": world, "batch_per_rank": a.batch, "dim": a.dim,
             "loss_symmetric": ls, "loss_allgather": la, "loss_fp32_torch": loss_ref,
-            "loss_rel_err_vs_fp32": lref_err,
+            "loss_rel_err_vs_fp32": lref_err, "runs": [f"{m}/{i}" for m, i in runs], "losses": losses,
+            "peak_mib_per_run_max_over_ranks": {f"{m}/{i}": round(max(p[8 + j] for p in per), 1)
+                                                for j, (m, i) in enumerate(runs)},
             "per_rank": [{"rank": i, "loss_rel_sym_vs_ag": p[0], "grad_err_sym_vs_ag": p[1],
                           "grad_err_sym_vs_fp32": p[6], "grad_err_ag_vs_fp32": p[7],
                           "peak_mib_symmetric": round(p[2], 1), "peak_mib_allgather": round(p[3], 1),
