@@ -118,6 +118,8 @@ class Engine {
   int nch_ = 1, nfull_ = 0;
   std::vector<std::pair<int, int>> segs_;  // (first, count) of each row chunk's cross tiles
   float2* part_x_ = nullptr;               // column partials of the cross tiles
+  float2* xsend_ = nullptr;                // packed column partials of the k-split block (one run per row tile
+  float2* xrecv_ = nullptr;                // otherwise: one send/recv per partner instead of one per row tile)
   char* mbuf_ = nullptr;                   // partners' mirrored coefficient blocks
   char* contrib_ = nullptr;                // partners' gradient contributions (nfull + split blocks)
   char* recv_ = nullptr;                   // received contributions [inc][Rpad][dim_n]

@@ -197,6 +197,19 @@ __device__ __forceinline__ void lds_get_inv(unsigned rbase, unsigned cbase, f32x
       : "v"(rbase), "v"(cbase), "i"(ROFS), "i"(ROFS + 64), "i"(ROFS + 128), "i"(ROFS + 192)
       : "memory");
 }
+// row inverse norms only (the second row half of an item: the column norms are the first half's)
+template <int ROFS>
+__device__ __forceinline__ void lds_get_rinv(unsigned rbase, f32x4 (&rs)[4]) {
+  asm volatile(
+      "ds_read_b128 %0, %4 offset:%c5\n\t"
+      "ds_read_b128 %1, %4 offset:%c6\n\t"
+      "ds_read_b128 %2, %4 offset:%c7\n\t"
+      "ds_read_b128 %3, %4 offset:%c8\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(rs[0]), "=&v"(rs[1]), "=&v"(rs[2]), "=&v"(rs[3])
+      : "v"(rbase), "i"(ROFS), "i"(ROFS + 64), "i"(ROFS + 128), "i"(ROFS + 192)
+      : "memory");
+}
 // fp8 operand row scales of one item (sim_gemm_kernel): 8 A dwords at abase + {0, 64, 128, 192,
 // 512, 576, 640, 704} and 4 B dwords at bbase + {0, 64, 512, 576}, one wait
 __device__ __forceinline__ void lds_get_scales(unsigned abase, unsigned bbase, unsigned (&av)[8], unsigned (&bv)[4]) {

@@ -1388,11 +1388,13 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
   // K-steps: no K halves) keep the stream-K split of the remainder.
   const int nstrip = fwd_diag_remainder(ntiles, nk_tile, cus, diag_tail, f8);
   // kDiagTickets arrival tickets per tile in the counter region (sized for any remainder below
-  // num_cus), 10 KS piece partials per tile in the slab region and 4 x 256 row-group partials per
-  // tile in the column-partial area (diag_up_kernel): every remainder of a whole-round launch fits
+  // num_cus), 10 KS piece partials per tile in the slab region and [4 row groups][4 slots][64 rows]
+  // float2 row-group partials per tile (8 KiB) in the column-partial area (diag_up_kernel's
+  // scratch; the area holds num_cus x kSkColpTile float2): every remainder of a whole-round launch fits
   NTXENT_CHECK((size_t)kDiagTickets * nstrip * 4 <= sk_counter_bytes(ws.num_cus) &&
                    (size_t)10 * kDiagKS * nstrip * 4096 <= (size_t)2 * ws.num_cus * kTileElems &&
-                   (size_t)nstrip * 4 * 64 * 4 <= (size_t)ws.num_cus * dev::kSkColpTile,
+                   (size_t)nstrip * dev::kDiagScratchTile * sizeof(float2) <=
+                       (size_t)ws.num_cus * dev::kSkColpTile * sizeof(float2),
                "diagonal remainder: workspace too small");
   const int nmain = ntiles - nstrip;
   const int pieces = part_x == nullptr ? fwd_splitk_pieces(ntiles, nk_tile, cus, diag_tail) : 0;
@@ -1437,8 +1439,6 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
     if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {
       if (nstrip > 0) {
-        // (a plain, short-lived grid: it does not keep ws.sched_cus CUs free; a transfer in flight
-        // gets CUs back as its blocks retire within the ~15 us launch)
         NTXENT_CHECK(p.A.kblk_stride == 0 && p.B.kblk_stride == 0, "diagonal remainder: row-major operands only");
         dev::SimParams q = p;
         q.tiles = tiles + nmain;
@@ -1453,15 +1453,19 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         static TimingBuf tb;
         q.tstamp = tb.prepare(nup, stream);
 #endif
+        // While a transfer is in flight (ws.sched_cus < num_cus) the region blocks are capped to
+        // the CUs the schedule leaves to compute and walk the regions (diag_up_kernel: nupg); the
+        // plain launch is one block per region
+        const int nupg = cus < ws.num_cus ? std::min(nup, cus) : nup;
         auto launch_up = [&](auto side, int nside) {
           using S = decltype(side);
-          const dim3 sg(nup + nside);
+          const dim3 sg(nupg + nside);
           if (diag_ks(nk_tile) == 2) {
-            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2, S>), sg, dim3(256), 0, stream, q, scratch, side);
-            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2, S>), sg, dim3(256), 0, stream, q, scratch, side);
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
           } else {
-            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1, S>), sg, dim3(256), 0, stream, q, scratch, side);
-            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1, S>), sg, dim3(256), 0, stream, q, scratch, side);
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
           }
         };
         using TS = typename dev::StoreT<Tc>::type;

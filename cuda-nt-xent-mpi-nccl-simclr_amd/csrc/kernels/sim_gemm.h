@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       const unsigned ib = (unsigned)(uintptr_t)(lds + kInvLds) + (unsigned)((item & 1) * 2048);
       // (cb[ni] = cb[0] + {0, 16, 128, 144}, rb[mi] = rb[0] + 16 (mi & 3) + 128 (mi >> 2))
       const unsigned rbase = ib + 4 * (rb[0] + 4 * (lane >> 4)), cbase = ib + 4 * (kTile + cb[0] + (lane & 15));
-      float cs[4], cs2[4];
+      float cs[4];
       f32x4 rs[4];
       auto scale4 = [&](int m0) {
 #pragma unroll
@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       };
       lds_get_inv<0>(rbase, cbase, rs, cs);
       scale4(0);
-      lds_get_inv<512>(rbase, cbase, rs, cs2);
+      lds_get_rinv<512>(rbase, rs);
       scale4(4);
     }
   }
@@ -1709,6 +1709,8 @@ constexpr int kSubStages = 3;
 // KS: K pieces of an off-diagonal region (a diagonal region gets KS / 2, at least 1); the pieces'
 // fp32 partials go to write-through slabs and the last piece to arrive (ticket) sums them in piece
 // order. 4 + 10 tickets and 10 KS 16 KiB slabs per tile (launch_fwd_stats checks the workspace).
+// row-group partial scratch of one diagonal tile: [4 row groups][4 contribution slots][64 rows] float2
+constexpr int kDiagScratchTile = 4 * 4 * 64;
 constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + column-partial exchange + flags
 // (diagonal regions in KS pieces as well: remainder 15.2 -> 16.4 us at the headline, the extra
 // piece merges cost more than the shorter K loop saves: profiles/r5/gemm_timing/diag_up.md)
@@ -1721,16 +1723,12 @@ struct NoSide {
   int nup;
   __device__ void operator()(int, int, char*) const {}
 };
-template <typename T, int FX, int KS, typename SIDE = NoSide>
-__global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch, const SIDE side) {
-  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
-  if ((int)blockIdx.x >= side.nup) {
-    side((int)blockIdx.x - side.nup, (int)gridDim.x - side.nup, smem);
-    return;
-  }
+template <typename T, int FX, int KS>
+__device__ __forceinline__ void diag_up_region(const SimParams& p, float2* __restrict__ scratch, const int nup,
+                                               const int vb, char* smem) {
 #if NTXENT_TIMING
   auto dmark = [&](int k) {
-    if (threadIdx.x == 0) p.tstamp[(long long)blockIdx.x * kTimingItems * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) p.tstamp[(long long)vb * kTimingItems * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
   };
 #else
   auto dmark = [](int) {};
@@ -1745,8 +1743,8 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int KSD = diag_ksd<KS>();                  // K pieces of a diagonal region
   constexpr int NB = diag_up_blocks<KS>();            // blocks per tile
-  const int nt_d = side.nup / NB;                    // diagonal tiles in this launch
-  const int idx = xcd_remap(blockIdx.x, side.nup);  // a tile's blocks share one XCD
+  const int nt_d = nup / NB;                    // diagonal tiles in this launch
+  const int idx = xcd_remap(vb, nup);          // a tile's blocks share one XCD
   const int tile = idx / NB, s = idx % NB;
   const bool dg = s < 4 * KSD;
   const int q = dg ? 0 : (s - 4 * KSD) / KS;                     // off-diagonal pair 0..5
@@ -1977,6 +1975,24 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
 #pragma unroll
   for (int kk = 1; kk < 4; ++kk) lse_merge(m, sm, __uint_as_float(qv[kk][0]), __uint_as_float(qv[kk][1]));
   p.part[(long long)nt * p.Rpad + r0 + 64 * g + lane] = make_float2(m, sm);
+}
+
+// nupg: blocks of the grid that run regions (the first nupg; the rest run the side job). Normally
+// nupg = side.nup, one block per region; while a transfer is in flight the launcher caps it to the
+// CUs the schedule leaves to compute (ws.sched_cus) and each block walks regions nupg apart: a
+// region's block never waits on another one (arrival tickets only), so any nupg >= 1 completes.
+template <typename T, int FX, int KS, typename SIDE = NoSide>
+__global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch, const SIDE side,
+                                                      const int nupg) {
+  __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
+  if ((int)blockIdx.x >= nupg) {
+    side((int)blockIdx.x - nupg, (int)gridDim.x - nupg, smem);
+    return;
+  }
+  for (int vb = (int)blockIdx.x; vb < side.nup; vb += nupg) {
+    diag_up_region<T, FX, KS>(p, scratch, side.nup, vb, smem);
+    __syncthreads();  // the next region restages the ring and the exchange area
+  }
 }
 
 // ------------------------------------------------------------------------------------

@@ -16,6 +16,16 @@
 #include "ntxent/trace.h"
 
 namespace ntxent {
+
+// float2 elements of the packed column-partial runs of the jobs whose partner row range is not a
+// whole block (k0 > 0 or k1 < row_tiles: the runs of consecutive row tiles are Rpad apart, not
+// adjacent), see Engine::forward_sym
+static size_t sym_xpack_floats2(const std::vector<SymJob>& jobs, int row_tiles) {
+  size_t n = 0;
+  for (const SymJob& j : jobs)
+    if (j.k1 - j.k0 != row_tiles) n += (size_t)(j.m1 - j.m0) * (j.k1 - j.k0) * kTile;
+  return n;
+}
 namespace {
 
 constexpr size_t kAlign = 256;
@@ -84,6 +94,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       // symmetric mode, fp32 plans: the received contributions follow the own slab (one stack)
       {(void**)&slabs_, Rp * g_.dim_n * 4 * (symm_ && ccs_ == 4 ? 1 + inc_.size() : 1)},
       {(void**)&part_x_, symm_ ? (size_t)g_.col_tiles * Rp * sizeof(float2) : 0},
+      {(void**)&xsend_, symm_ ? sym_xpack_floats2(jobs_, g_.row_tiles) * sizeof(float2) : 0},
+      {(void**)&xrecv_, symm_ ? sym_xpack_floats2(inc_, g_.row_tiles) * sizeof(float2) : 0},
       {(void**)&mbuf_, symm_ ? (size_t)std::max(1, world_ / 2) * g_.row_tiles * g_.row_tiles * kTileElems * cs_ : 0},
       {(void**)&contrib_, symm_ ? (jobs_.size() + 1) * Rp * g_.dim_n * ccs_ : 0},
       {(void**)&recv_, symm_ && ccs_ == 2 ? inc_.size() * Rp * g_.dim_n * ccs_ : 0},

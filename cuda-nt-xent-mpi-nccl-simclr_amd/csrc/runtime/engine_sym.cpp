@@ -153,21 +153,48 @@ void Engine::forward_sym(const void* h, hipStream_t s) {
   if (f8_) NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_f16_, 0));
   {
     // column partials of the cross tiles -> their rows' owners: rank q's part slots
-    // [r * rt + m] for its rows [k0, k1) (one contiguous run per row tile m)
+    // [r * rt + m] for its rows [k0, k1), one run per row tile m, Rpad apart. A whole-block job
+    // (k0 = 0, k1 = rt) has its runs back to back: ONE send / recv. The k-split block's runs are
+    // packed into xsend_ (one 2-D copy) and unpacked from xrecv_ after the exchange: one op per
+    // partner instead of one per row tile (W = 8: 224 -> 8 RCCL ops per step; each op costs the
+    // host several microseconds inside the group call).
     NTXENT_TRACE("ntxent.fwd_col_partials");
     std::vector<P2POp> ops;
-    const size_t run = sizeof(float2) * kTile;
-    for (const SymJob& j : jobs_)
-      for (int m = j.m0; m < j.m1; ++m)
-        ops.push_back({true, part_x_ + ((size_t)(j.q * rt + m) * Rp + (size_t)j.k0 * kTile), (size_t)(j.k1 - j.k0) * run, j.q});
-    for (const SymJob& p : inc_)
-      for (int m = p.m0; m < p.m1; ++m)
-        ops.push_back({false, part_ + ((size_t)(p.q * rt + m) * Rp + (size_t)p.k0 * kTile), (size_t)(p.k1 - p.k0) * run, p.q});
+    const size_t f2 = sizeof(float2);
+    struct Unpack { float2* dst; const float2* src; size_t run; int rows; };
+    std::vector<Unpack> unpack;
+    size_t so = 0, ro = 0;
+    for (const SymJob& j : jobs_) {
+      const size_t run = (size_t)(j.k1 - j.k0) * kTile;  // float2 per row tile
+      float2* first = part_x_ + ((size_t)(j.q * rt + j.m0) * Rp + (size_t)j.k0 * kTile);
+      const int nm = j.m1 - j.m0;
+      if (run == Rp) {
+        ops.push_back({true, first, (size_t)nm * Rp * f2, j.q});
+      } else {
+        NTXENT_HIP_CHECK(hipMemcpy2DAsync(xsend_ + so, run * f2, first, Rp * f2, run * f2, nm, hipMemcpyDeviceToDevice, s));
+        ops.push_back({true, xsend_ + so, (size_t)nm * run * f2, j.q});
+        so += (size_t)nm * run;
+      }
+    }
+    for (const SymJob& p : inc_) {
+      const size_t run = (size_t)(p.k1 - p.k0) * kTile;
+      float2* first = part_ + ((size_t)(p.q * rt + p.m0) * Rp + (size_t)p.k0 * kTile);
+      const int nm = p.m1 - p.m0;
+      if (run == Rp) {
+        ops.push_back({false, first, (size_t)nm * Rp * f2, p.q});
+      } else {
+        ops.push_back({false, xrecv_ + ro, (size_t)nm * run * f2, p.q});
+        unpack.push_back({first, xrecv_ + ro, run, nm});
+        ro += (size_t)nm * run;
+      }
+    }
     NTXENT_HIP_CHECK(hipEventRecord(ev_x_, s));
     NTXENT_HIP_CHECK(hipStreamWaitEvent(comm_stream_, ev_x_, 0));
     comm_->send_recv(ops, comm_stream_);
     NTXENT_HIP_CHECK(hipEventRecord(ev_xdone_, comm_stream_));
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_xdone_, 0));
+    for (const Unpack& u : unpack)
+      NTXENT_HIP_CHECK(hipMemcpy2DAsync(u.dst, Rp * f2, u.src, u.run * f2, u.run * f2, u.rows, hipMemcpyDeviceToDevice, s));
   }
   {
     NTXENT_TRACE("ntxent.lse");

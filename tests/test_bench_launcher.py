@@ -7,6 +7,7 @@ rendezvous, timing brackets, rank-max reduction and JSON assembly are the same c
 run uses.
 """
 import json
+import math
 import os
 import subprocess
 import sys
@@ -38,6 +39,10 @@ def test_launcher_spawns_ranks_and_relays_one_json_line(n, negatives):
     assert d["value"] == pytest.approx(n * 16 / (d["ms_per_step"] / 1e3), rel=1e-3)
     assert len(d["comm_wait_ms_per_step_per_rank"]) == n
     assert d["loss"] == d["loss"]  # finite
+    # host cost of the multi-rank step (verdict r5: the N > 1 step must be shown GPU-bound)
+    he = d["host_enqueue_ms_per_step"]
+    assert isinstance(he, float) and math.isfinite(he) and he > 0.0, he
+    assert d["config"]["dist_impl"] in (None, "engine", "torch")
 
 
 def test_rank_failure_fails_the_job():

@@ -65,3 +65,55 @@ def test_side_job_zt_gradient_matches_unit_row_path(ext):
         ext.set_raw_forward(old)
     scale = grads[1].abs().max().item()
     assert (grads[0] - grads[1]).abs().max().item() <= 1e-2 * scale
+
+
+def _low_loss_views(rows, dim, rank, noise, seed):
+    # views of points on a rank-`rank` subspace: positives nearly identical, the nearest negatives
+    # close enough that tau = 0.01 leaves a small but nonzero loss (~0.04 at rank 8, noise 0.1)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    n = rows // 2
+    basis = torch.randn(rank, dim, device="cuda", generator=g, dtype=torch.float64)
+    base = torch.randn(n, rank, device="cuda", generator=g, dtype=torch.float64) @ basis / rank**0.5
+    v1 = base + noise * torch.randn(n, dim, device="cuda", generator=g, dtype=torch.float64)
+    v2 = base + noise * torch.randn(n, dim, device="cuda", generator=g, dtype=torch.float64)
+    return torch.cat([v1, v2], 0).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("rows,dim", [(16384, 128), (16384, 512)])
+def test_ticket_loss_low_loss_low_tau(ext, rows, dim):
+    # the regime where the fixed-point quantum (sized from the worst-case bound log 2N + 2/tau + 1
+    # per row) is largest relative to the sum: tau = 0.01, strongly correlated views, loss < 0.05
+    import ntxent_amd
+
+    h = _low_loss_views(rows, dim, rank=8, noise=0.1, seed=rows + dim)
+    ref = R.ntxent_loss(h.double(), 0.01).item()
+    assert 1e-4 < ref < 0.05, ref
+    a = ntxent_amd.ntxent_loss(h, 0.01).item()
+    assert a == ntxent_amd.ntxent_loss(h, 0.01).item()
+    assert abs(a - ref) <= 1e-6 * abs(ref), (a, ref, abs(a - ref) / ref)
+
+
+@pytest.mark.parametrize("raw", [True, False])
+def test_zt_exact_against_unit_rows(ext, raw):
+    # Z^T (the dZ GEMM's B operand) element-wise: the raw-operand forward's side job (DiagSideZt,
+    # beside the diagonal remainder at 8192 x 2048) writes fp16((h * inv)^T) from the returned inv;
+    # the unit-row forward's LSE-launch transpose writes zq^T. Exact, padded rows/columns zero.
+    h = _views(8192, 2048, seed=5)
+    old = ext.raw_forward_enabled()
+    try:
+        ext.set_raw_forward(raw)
+        out = ext.fused_forward(h, 0.07, "fp16", True)
+    finally:
+        ext.set_raw_forward(old)
+    zq, zqt, inv = out[1], out[2], out[3]
+    rows, dim = h.shape
+    assert zqt.dtype == torch.float16 and zqt.shape[0] >= dim and zqt.shape[1] >= rows
+    if raw:
+        assert zq.numel() == 0  # nothing reads unit rows on the raw path
+        want = (h.float() * inv[:, None]).to(torch.float16).t()
+    else:
+        want = zq[:rows, :dim].t()
+    got = zqt[:dim, :rows]
+    bad = (got != want).sum().item()
+    assert bad == 0, f"{bad} mismatching Z^T elements, max diff {(got.float() - want.float()).abs().max().item()}"
+    assert (zqt[dim:] == 0).all().item()

@@ -105,13 +105,15 @@ def test_per_tile_max_epilogue_at_scale(ext, compute):
     assert lerr <= lt and gerr <= gt, (lerr, gerr)
 
 
-@pytest.mark.parametrize("reserve", [8, 37])
-def test_grid_reserve_same_result(ext, reserve):
+@pytest.mark.parametrize("reserve,dim", [(8, 1024), (37, 1024), (8, 2048)])
+def test_grid_reserve_same_result(ext, reserve, dim):
     """GEMMs launched with CUs left for communication (reserve_cus: a 248- or 219-block persistent
     grid, so a different stream-K split) agree with the full grid to fp32 summation-order
-    rounding: forward partials (fwd_stats_range) and the dZ (dz_view)."""
-    h = _views(8192, 1024, seed=4)
-    plan = ext.get_plan(8192, 1024, 1, 0, 0.07, "fp16", 0)
+    rounding: forward partials (fwd_stats_range) and the dZ (dz_view). Reserve 8 at 8192 rows
+    leaves a 32-tile diagonal remainder (512 region blocks) that the capped diag_up grid (248
+    blocks) walks in three passes."""
+    h = _views(8192, dim, seed=4)
+    plan = ext.get_plan(8192, dim, 1, 0, 0.07, "fp16", 0)
     zq, inv, ypos, _ = ext.prep(h, plan)
     outs = []
     for res in (0, reserve):

@@ -3,7 +3,7 @@
 # failure is listed), bench.py x2, rocprofv3 kernel stats of bench.py, native bench at the
 # BASELINE configs. usage: tools/gpu_check.sh TAG [skip-tests]
 set -o pipefail
-export TMPDIR=/tmp
+export TMPDIR=/tmp NTXENT_GPU_CHECK=1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-check}; mkdir -p $OUT
 timeout -k 10 400 build/bin/ntxent_tests > $OUT/cpp_tests.log 2>&1 || { echo "cpp tests failed"; tail -30 $OUT/cpp_tests.log; exit 1; }
 tail -1 $OUT/cpp_tests.log

@@ -1,20 +1,27 @@
 #!/bin/bash
-# Round 6, verdict item 1/2: the data-parallel step's host cost and the config-3 shape on one GPU.
-#   1. the RCCL multi-process tests (engine and torch implementations) + the config-3 W = 4 test
-#   2. bench.py --gpus N --backend nccl --share-gpu at B = 4096, d = 2048 for N = 2, 4, 8, both
-#      negatives modes, dist-impl engine (the default) and torch: host_enqueue_ms_per_step
-#   3. cProfile of the torch symmetric path's host side at N = 8 (where its time goes)
-# usage: tools/gpu_r6_dist.sh TAG
+# Round 6, verdict items 1/2: the data-parallel step's host cost and the config-3 shape on one GPU.
+#   1. pytest selection ($2, default: the RCCL multi-process tests incl. the config-3 W = 4 test)
+#   2. bench.py (N = 1) twice: headline regression check
+#   3. bench.py --gpus N --backend nccl --share-gpu at B = 4096, d = 2048 for N in $3 (default
+#      "2 8"), both negatives modes, dist-impl engine (the default) and torch:
+#      host_enqueue_ms_per_step; cProfile of the torch path's host side at N = 8
+# usage: tools/gpu_r6_dist.sh TAG [PYTEST_ARGS] [NS]
 set -o pipefail
-export TMPDIR=/tmp
+export TMPDIR=/tmp NTXENT_GPU_CHECK=1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6dist}; mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests/test_gpu_multiproc.py -k "rccl" -v -rA --durations 10 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest_rccl.log 2>&1
+SEL=${2:-"tests/test_gpu_multiproc.py -k rccl"}
+NS=${3:-"2 8"}
+timeout -k 10 900 python -u -m pytest $SEL -v -rA --durations 10 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
 rc=$?
-grep -E "passed|failed" $OUT/pytest_rccl.log | tail -2
-grep -E "^(FAILED|ERROR)" $OUT/pytest_rccl.log | head -30
+grep -E "passed|failed" $OUT/pytest.log | tail -2
+grep -E "^(FAILED|ERROR)" $OUT/pytest.log | head -30
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest aborted rc=$rc"; exit 1; fi
+for i in 1 2; do
+timeout -k 10 200 python bench.py > $OUT/bench$i.log 2>&1 || { echo "bench failed"; tail $OUT/bench$i.log; exit 1; }
+tail -1 $OUT/bench$i.log | cut -c1-200
+done
 B="--batch 4096 --dim 2048 --steps 5 --warmup 1 --prewarm-steps 2 --backend nccl --share-gpu --timeout 280"
-for N in 2 4 8; do
+for N in $NS; do
   for neg in symmetric allgather; do
     for impl in engine torch; do
       hp=""

@@ -173,7 +173,9 @@ def main():
     ok = True
     if rank == 0:
         per = [r.tolist() for r in allrows]
-        worst_grad = max(max(p[1], p[6], p[7]) for p in per)
+        # each mode within grad_tol of the fp32 oracle; symmetric vs all-gather (two independent bf16
+        # roundings of the gradient) within twice that
+        worst_grad = max(max(p[1] / 2, p[6], p[7]) for p in per)
         worst_loss = max(p[0] for p in per)
         nr = len(runs)
         losses = {f"{m}/{i}": per[0][8 + nr + j] for j, (m, i) in enumerate(runs)}
