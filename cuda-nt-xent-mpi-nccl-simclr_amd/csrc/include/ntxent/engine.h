@@ -118,6 +118,8 @@ class Engine {
   int nch_ = 1, nfull_ = 0;
   std::vector<std::pair<int, int>> segs_;  // (first, count) of each row chunk's cross tiles
   float2* part_x_ = nullptr;               // column partials of the cross tiles
+  float2* fold_pre_ = nullptr;             // folded LSE scratch (RawRows::fold_pre / fold_cnt)
+  int* fold_cnt_ = nullptr;
   float2* xsend_ = nullptr;                // packed column partials of the k-split block (one run per row tile
   float2* xrecv_ = nullptr;                // otherwise: one send/recv per partner instead of one per row tile)
   char* mbuf_ = nullptr;                   // partners' mirrored coefficient blocks

@@ -214,7 +214,20 @@ struct RawRows {
   const float* inv = nullptr;   // [rows] 1 / |h_i|
   void* zqt = nullptr;          // [dim_n][ld_t] Z^T in `zt` (the plan's backward dtype), or null
   DType zt = DType::F16;
+  // Optional: the LSE launch's outputs (launch_lse's arguments). When set and the diagonal
+  // remainder is exactly the second half's diagonal tiles (with Z^T beside it), the remainder
+  // launch computes them itself (LseFold) and sets lse_folded: the caller then skips launch_lse.
+  const float* ypos = nullptr;
+  float* lse2 = nullptr;
+  float* cpos = nullptr;
+  float* block_loss = nullptr;
+  float* loss = nullptr;
+  float2* fold_pre = nullptr;   // [Rpad] scratch of the folded LSE (pre-merged row states)
+  int* fold_cnt = nullptr;      // [Rpad / 64] zeroed counters (self-cleaning)
+  mutable bool lse_folded = false;
 };
+void set_lse_fold(bool on);  // default: NTXENT_LSE_FOLD (unset: on)
+bool lse_fold_enabled();
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp);  // world 1, 2-byte in & comp, rows % 256, dim % 64
 void set_raw_forward(bool on);  // default on (off: the zq path, for A/B and tests)
 bool raw_forward_enabled();
@@ -291,7 +304,9 @@ int dot_slots(const Geometry& g);
 // the partials of the dequantised coefficients (plus the exact positive term).
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf = nullptr, float* dotp = nullptr, const Q8Stats* q8 = nullptr);
+                 void* mbuf = nullptr, float* dotp = nullptr, const Q8Stats* q8 = nullptr, bool half_c = false);
+// half_c: write only the upper coefficient tiles (an off-diagonal tile's mirror is skipped; the
+// dZ launched with half_c reads C_IJ, J < I, as C_JI^T). Only with dz_half_c_eligible.
 // dot[Rpad] = row sums of dotp.
 void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream);
 
@@ -324,10 +339,16 @@ struct NormFuse {
 // block-scaled MFMA, per-row dequantisation and the exact positive term in the epilogue).
 bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* tiles, int ntiles,
                void* dz, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16 = false,
-               const NormFuse* nf = nullptr, const Q8Stats* q8 = nullptr, const float* cpos = nullptr);
-
-// (A dZ that reads only the upper-triangular C, mirrored K-steps and Z through transposed LDS reads,
-// measured 33 us slower than the mirrored C + Z^T path at the headline: profiles/r3/dzexp.)
+               const NormFuse* nf = nullptr, const Q8Stats* q8 = nullptr, const float* cpos = nullptr,
+               bool half_c = false);
+// Half C (SimParams::c_half): the coefficient pass writes the upper tiles only and the dZ stages a
+// lower K tile C_IJ (J < I) from C_JI through a transposing LDS image (ds_read_b64_tr_b16, one
+// lane base per wave). Needs a 16-bit backward, one rank and whole-tile dZ items (the schedule of
+// launch_dz: no split-K, no stream-K remainder). (Round 3's dz_sym also read Z through transposed
+// LDS reads, 33 us slower at the headline, ~10 us of it the mirrored A K-steps: profiles/r3/dzexp.)
+bool dz_half_c_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace& ws);
+void set_half_c(bool on);  // default: NTXENT_HALF_C (unset: on)
+bool half_c_enabled();
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first

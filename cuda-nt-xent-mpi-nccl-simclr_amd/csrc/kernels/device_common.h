@@ -293,6 +293,18 @@ __device__ __forceinline__ int q8_row_exp(float mneg2, float lmin) {
 }
 __device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }  // |e| <= 126
 
+// Row statistics from a row's merged negatives-only (max, sum) state: returns lse2 and writes
+// the natural-log loss term softplus(lse_neg - y_pos) and a = 1 - P_ip = sigmoid(lse_neg - y_pos).
+__device__ __forceinline__ float finish_row(float m, float s, float yp, float& loss, float& a) {
+  const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
+  const float mx = fmaxf(neg2, yp);  // lse = logaddexp(lse_neg, y_pos)
+  const float l2 = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
+  const float x = (neg2 - yp) * kLn2;
+  loss = x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
+  a = 1.0f / (1.0f + exp2f(yp - neg2));
+  return l2;
+}
+
 // Block-wide sum for up to 1024 threads; `red` must hold >= 16 floats. All threads get it.
 __device__ __forceinline__ float block_sum(float x, float* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -517,17 +517,6 @@ __global__ __launch_bounds__(256) void transpose_kernel(const T* __restrict__ zq
   transpose_tile<T>(zq, zqt, dk, ldk, ldt, blockIdx.x, blockIdx.y, tile);
 }
 
-// Row statistics from a row's merged negatives-only (max, sum) state: returns lse2 and writes
-// the natural-log loss term softplus(lse_neg - y_pos) and a = 1 - P_ip = sigmoid(lse_neg - y_pos).
-__device__ __forceinline__ float finish_row(float m, float s, float yp, float& loss, float& a) {
-  const float neg2 = (m == kNegInf || s <= 0.f) ? kNegInf : m + log2f(s);
-  const float mx = fmaxf(neg2, yp);  // lse = logaddexp(lse_neg, y_pos)
-  const float l2 = mx + log2f(exp2f(neg2 - mx) + exp2f(yp - mx));
-  const float x = (neg2 - yp) * kLn2;
-  loss = x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
-  a = 1.0f / (1.0f + exp2f(yp - neg2));
-  return l2;
-}
 
 // Eight lanes per positive pair (i, i+n): lane q merges column tiles q, q+8, ... of both rows,
 // an xor-shuffle tree merges the eight states, lane 0 finishes: LSE of both rows, their loss
@@ -798,34 +787,35 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(const float* __restrict__
 }
 
 // dot_i = sum over the coefficient pass's slots dotp[k][i] (slot-major; fixed order: deterministic).
-// 4 threads per row (slots q, q + 4, ...; 32 or 8 loads in flight each, summed in slot order),
-// 64 rows per block: the loads of a wave cover 16 consecutive rows of 4 slots.
+// 32 rows per block (one per CU at the headline: 256 blocks), 8 threads per row: thread (w, lane)
+// takes row (lane & 31) and slots sg, sg + 8, ... (sg = 2 w + (lane >> 5)), all its loads in flight
+// at once; the 8 partials are then summed in sg order. (64 rows x 4 slot groups per block left half
+// the CUs idle and put 32 loads behind each thread: 5.0 us at the headline.)
 __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict__ dotp, int nslot, int rows,
                                                          float* __restrict__ dot) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
-  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 32 + (lane & 31), sg = 2 * w + (lane >> 5);
+  __shared__ float part[8][32];
   float s = 0.f;
   if (i < rows) {
-    int k = q;
-    for (; k + 124 < nslot; k += 128) {  // 32 loads in flight (config 5, 256 slots: 8.0 -> 6.1 us)
-      float v[32];
+    int k = sg;
+    for (; k + 120 < nslot; k += 128) {  // 16 loads in flight
+      float v[16];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) v[u] = dotp[(long long)(k + 4 * u) * rows + i];
+      for (int u = 0; u < 16; ++u) v[u] = dotp[(long long)(k + 8 * u) * rows + i];
 #pragma unroll
-      for (int u = 0; u < 32; ++u) s += v[u];
+      for (int u = 0; u < 16; ++u) s += v[u];
     }
-    for (; k + 28 < nslot; k += 32) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = dotp[(long long)(k + 4 * u) * rows + i];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; k < nslot; k += 4) s += dotp[(long long)k * rows + i];
+    for (; k < nslot; k += 8) s += dotp[(long long)k * rows + i];
   }
-  part[q][threadIdx.x & 63] = s;
+  part[sg][lane & 31] = s;
   __syncthreads();
-  if (q == 0 && i < rows) dot[i] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
+  if (threadIdx.x < 32 && blockIdx.x * 32 + (int)threadIdx.x < rows) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += part[g][threadIdx.x];
+    dot[blockIdx.x * 32 + threadIdx.x] = t;
+  }
 }
 
 }  // namespace dev
@@ -1309,6 +1299,35 @@ void set_small_fuse_rows(int rows) { g_small_fuse_rows = rows < 0 ? -1 : rows; }
 int small_fuse_rows_override() { return g_small_fuse_rows.load(); }
 void set_fp8_backward(bool on) { g_fp8_bwd = on; }
 void set_raw_forward(bool on) { g_raw_fwd = on; }
+
+static std::atomic<bool> g_lse_fold{[] {
+  const char* e = std::getenv("NTXENT_LSE_FOLD");
+  return e == nullptr || std::string(e) != "0";
+}()};
+void set_lse_fold(bool on) { g_lse_fold = on; }
+bool lse_fold_enabled() { return g_lse_fold.load(); }
+static double lse_loss_fx(const Geometry& g, int nb);
+
+static std::atomic<bool> g_half_c{[] {
+  const char* e = std::getenv("NTXENT_HALF_C");
+  return e == nullptr || std::string(e) != "0";
+}()};
+void set_half_c(bool on) { g_half_c = on; }
+bool half_c_enabled() { return g_half_c.load(); }
+
+// The scheduling decisions of launch_dz, replayed: half C needs every dZ item to start at an even
+// K-step (whole tiles, or split-K pieces of an even ipb), so that an item's lower-tile K-steps
+// (4 per tile) are an even count ahead of its upper ones; stream-K ranges are arbitrary.
+bool dz_half_c_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace& ws) {
+  if ((comp != DType::F16 && comp != DType::BF16) || g.world != 1 || n_dz <= 0) return false;
+  if ((long long)g.row_tiles * g.col_tiles * kTileElems * 2 >= (1ll << 31)) return false;  // 32-bit offsets
+  const int cus = ws.sched_cus > 0 ? std::min(ws.sched_cus, ws.num_cus) : ws.num_cus;
+  const int nk = (int)((long long)g.rows_pad * 2 / kKStepBytes);
+  int pieces = fwd_splitk_pieces(n_dz, nk, cus, 1);
+  if (pieces < 3) pieces = 0;
+  if (pieces > 0) return ((nk + pieces - 1) / pieces) % 2 == 0;
+  return make_schedule(n_dz, nk, cus).sk_tiles == 0;
+}
 bool raw_forward_enabled() { return g_raw_fwd.load(); }
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp) {
   // (fp16 rows on a bf16 plan would keep fp16 cosines for a bf16 backward: not offered)
@@ -1457,15 +1476,41 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
         // the CUs the schedule leaves to compute and walk the regions (diag_up_kernel: nupg); the
         // plain launch is one block per region
         const int nupg = cus < ws.num_cus ? std::min(nup, cus) : nup;
+        // the LSE launch folded into this one (LseFold): the remainder = the diagonal tiles of
+        // exactly the second half of the rows, Z^T beside it, raw rows (world 1, R = Rpad)
+        dev::LseFold lf{};
+        const int nhalf = g.rows / 2;
+        // (the launch is build_fwd_tiles' whole own block: its diagonal tiles come last, in panel
+        // order, so the remainder is panels [rt - nstrip, rt))
+        if (raw && raw->lse2 && raw->zqt && raw->fold_pre && raw->fold_cnt && lse_fold_enabled() && nup <= ws.num_cus &&
+            g.world == 1 &&
+            g.rows == g.rows_pad && nhalf % kTile == 0 && nstrip * kTile == nhalf && diag_tail == g.row_tiles &&
+            ntiles == count_own_fwd_tiles(g)) {
+          {
+            lf.on = 1;
+            lf.n = nhalf;
+            lf.ngroups = nstrip * 4;
+            lf.ypos = raw->ypos;
+            lf.lse2 = raw->lse2;
+            lf.cpos = raw->cpos;
+            lf.ticket = reinterpret_cast<unsigned long long*>(raw->block_loss + 2);
+            lf.loss = raw->loss;
+            lf.pre = raw->fold_pre;
+            lf.gcnt = raw->fold_cnt;
+            lf.loss_scale = (float)(1.0 / (double)g.global_rows);
+            lf.loss_fx = lse_loss_fx(g, lf.ngroups);
+            NTXENT_CHECK(lf.loss_fx > 0.0, "lse fold: ticket scale");
+          }
+        }
         auto launch_up = [&](auto side, int nside) {
           using S = decltype(side);
           const dim3 sg(nupg + nside);
           if (diag_ks(nk_tile) == 2) {
-            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
-            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg, lf);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 2, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg, lf);
           } else {
-            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
-            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg);
+            if (p.fixed_shift) hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 1, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg, lf);
+            else hipLaunchKernelGGL((dev::diag_up_kernel<Tc, 0, 1, S>), sg, dim3(256), 0, stream, q, scratch, side, nupg, lf);
           }
         };
         using TS = typename dev::StoreT<Tc>::type;
@@ -1488,12 +1533,18 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
             zs.ldt = (int)g.ld_t;
             zs.tx = g.rows_pad / 64;
             zs.ntiles = zs.tx * (g.dim_n / 64);  // (rows [dim, dim_n) of Z^T: zeros)
-            launch_up(zs, std::min(zs.ntiles, NTXENT_ZT_SIDE_PER_CU * ws.num_cus));
+            const int nside = std::min(zs.ntiles, NTXENT_ZT_SIDE_PER_CU * ws.num_cus);
+            if (4 * nside < lf.ngroups) lf.on = 0;  // (every group needs its pre-merging side wave)
+            launch_up(zs, nside);
             side_zt = true;
           }
         }
-        if (!side_zt) launch_up(dev::NoSide{nup}, 0);
+        if (!side_zt) {
+          lf.on = 0;  // (the LSE launch still runs: it writes Z^T)
+          launch_up(dev::NoSide{nup}, 0);
+        }
         zt_done = side_zt;
+        if (raw) raw->lse_folded = side_zt && lf.on;
 #if NTXENT_TIMING
         tb.dump("diag_up", nup, stream);
 #endif
@@ -1596,9 +1647,12 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf, float* dotp, const Q8Stats* q8) {
+                 void* mbuf, float* dotp, const Q8Stats* q8, bool half_c) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
+  NTXENT_CHECK(!half_c || (mbuf == nullptr && q8 == nullptr && g.world == 1 && (comp == DType::F16 || comp == DType::BF16)),
+               "coef: half C needs a 16-bit, single-rank, mirrored-layout pass");
+  p.c_half = half_c ? 1 : 0;
   p.dotp = dotp;
   p.tiles = tiles;
   p.sc = const_cast<char*>(static_cast<const char*>(sbuf));
@@ -1629,7 +1683,7 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
 int dot_slots(const Geometry& g) { return 4 * g.col_tiles; }
 
 void launch_dot_reduce(const float* dotp, float* dot, const Geometry& g, hipStream_t stream) {
-  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 63) / 64), dim3(256), 0, stream, dotp, dot_slots(g),
+  hipLaunchKernelGGL(dev::dot_reduce_kernel, dim3((g.rows_pad + 31) / 32), dim3(256), 0, stream, dotp, dot_slots(g),
                      g.rows_pad, dot);
   NTXENT_HIP_CHECK(hipGetLastError());
 }
@@ -1653,8 +1707,9 @@ static bool apply_norm_fuse(dev::SimParams& p, const NormFuse* nf, const Geometr
 
 bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tiles, int ntiles,
                void* slabs, const GemmWorkspace& ws, const Geometry& g, hipStream_t stream, bool out_f16,
-               const NormFuse* nf, const Q8Stats* q8, const float* cpos) {
+               const NormFuse* nf, const Q8Stats* q8, const float* cpos, bool half_c) {
   if (ntiles == 0) return false;
+  NTXENT_CHECK(!half_c || dz_half_c_eligible(comp, g, ntiles, ws), "dz: half C not eligible for this launch");
   const bool f8 = comp == DType::FP8;
   NTXENT_CHECK(!f8 || (q8 && q8->mneg2 && q8->lmin && q8->zq && cpos && g.world == 1 && out_f16),
                "dz (fp8 backward): Q8Stats, cpos, world 1 and an fp16 slab required");
@@ -1707,6 +1762,11 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   } else {
     grid = apply_schedule(p, ntiles, ws, stream);
   }
+  if (half_c)
+    NTXENT_CHECK(((pieces == 0 && p.sk_tiles == 0 && p.dp_tiles == ntiles) || (pieces > 0 && p.ipb % 2 == 0)) &&
+                     (long long)g.row_tiles * g.col_tiles * kTileElems * cs < (1ll << 31),
+                 "dz: half C needs items starting at even K-steps and a C buffer below 2 GiB (32-bit offsets)");
+  p.c_half = half_c ? 1 : 0;
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
   if (fused) NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot");
   dispatch_gemm(comp, [&](auto tc) {

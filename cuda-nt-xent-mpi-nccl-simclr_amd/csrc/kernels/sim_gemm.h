@@ -92,6 +92,11 @@ struct SimParams {
   int b_tile0;           // B operand: global column tile of the chunk's first row tile (ring mode)
   int c_ld, c_tile0;     // coefficient tile slot = mt * c_ld + (nt - c_tile0)
   int c_rot;             // symmetric mode: column slot (nt - row_tile0) mod col_tiles instead (sym_c_ld)
+  // half C (world 1, 16-bit, whole-tile dZ items): the coefficient pass writes only the upper
+  // tiles (J >= I; no mirror of an off-diagonal tile) and the dZ reads a lower tile C_IJ (J < I)
+  // as the transpose of C_JI (dz_tr_stage / ds_read_b64_tr_b16): 64 MiB fewer C bytes written at
+  // the headline
+  int c_half;
   // raw-operand forward (RawRows): A / B are the input rows h, not unit rows; the accumulators are
   // normalised by inv_a[A row] * inv_b[B row] before the epilogue (null: unit-row operands)
   const float* inv_a;
@@ -158,14 +163,17 @@ __device__ __forceinline__ int sc_unit(int rb, int cb, int lane) { return ((rb >
 struct KStream {
   const char* ptr;  // the K-step to stage next
   int kin, left;    // byte offset inside its K block; K-steps after it
+  int kk;           // K-step index (of the whole K range) of ptr
   __device__ __forceinline__ void init(const char* base, long long k0, const OperandDesc& o, int nk) {
     kin = (int)(k0 % o.kblk);
     ptr = base + (k0 / o.kblk) * o.kblk_stride + kin;
     left = nk - 1;
+    kk = (int)(k0 / kKStepBytes);
   }
   __device__ __forceinline__ void advance(const OperandDesc& o) {
     if (left > 0) {
       --left;
+      ++kk;
       ptr += kKStepBytes;
       kin += kKStepBytes;
       if (kin == o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }
@@ -241,7 +249,8 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
   }
   T* slot = base + ctile_index(p, mt, nt) * kTileElems;
   T* mirror = nullptr;
-  if (kind == kTileSymOff || kind == kTileDiagUp)  // (kTileDiagUp: the same tile's slot)
+  // (kTileDiagUp: the same tile's slot; half C: no lower off-diagonal tiles, the dZ reads C_JI^T)
+  if ((kind == kTileSymOff && !p.c_half) || kind == kTileDiagUp)
     mirror = base + ctile_index(p, nt - p.row_tile0, p.row_tile0 + mt) * kTileElems;
   else if (kind == kTileCross) {  // partner block C_{q,rank}: mbuf tile (slot, nt % rt, mt)
     const int rt = p.Rpad / kTile, W = p.col_tiles / rt, q = nt / rt;
@@ -970,11 +979,47 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     a_vo[j] = (unsigned)((lane >> 3) * p.A.ld) + lchunk * 16;
     b_vo[j] = (unsigned)((lane >> 3) * p.B.ld) + lchunk * 16;
   }
+  // Half C (p.c_half, 16-bit dZ): the item's K-steps below tr_end (its row panel I's lower tiles
+  // J < I) are staged from C_JI, which the coefficient pass wrote instead of C_IJ. Half-tile h of
+  // K-step kk = rows kc .. kc + 63 (kc = 64 (kk & 3)) of tile (J = kk >> 2, I), bytes 256 h ..
+  // 256 h + 255 of each 512-byte row: 16 pieces of 4 rows, wave w issuing pieces 2 w, 2 w + 1.
+  // 16-B slot L of piece P holds row q = (L >> 1) & 3, chunk ch = 8 (((L >> 3) & 1) ^ x) +
+  // 2 (L >> 4) + (L & 1), x = (P >> 1) & 1 (= w & 1): the transposed reads of read_a_tr are then
+  // bank-conflict-free (a 32-lane half's two 4-row blocks sit in opposite 32-bank halves) and every
+  // one of them is ONE lane base + an immediate (the 16-column block index lands in slot bits 4-5).
+  constexpr bool kTrCap = MODE == kModeDz && sizeof(T) == 2 && !std::is_same<T, fp8e4m3>::value;
+  int tr_end = 0;               // (set per item by the prologue)
+  const char* tr_base = nullptr;  // tile (0, I) of the item's row panel I
+  unsigned a_tr_vo = 0, rd_tr = 0;
+  if constexpr (kTrCap) {
+    const int x = w & 1;
+    const int ch = 8 * (((lane >> 3) & 1) ^ x) + 2 * (lane >> 4) + (lane & 1);
+    a_tr_vo = (unsigned)(((lane >> 1) & 3) * p.A.ld + 16 * ch);
+    // read side: lane 4 q + pp of 16-lane group g supplies row q, columns 4 pp .. 4 pp + 3 of the
+    // block (ds_read_b64_tr_b16): piece 8 s + 2 g + hi, slot 16 mi + 8 (wa ^ (g & 1)) + 2 q + (pp >> 1)
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    rd_tr = (unsigned)(2048 * g + 128 * (wa ^ (g & 1)) + 32 * q + 16 * (pp >> 1) + 8 * (pp & 1));
+    asm volatile("" : "+v"(a_tr_vo), "+v"(rd_tr));
+  }
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
   auto stage = [&](int isB, int h, KStream& s, int buf) {
     // LDS layout [A even | A odd | B even | B odd] (32 KiB each): every operand read of either
     // parity is its lane base + a 16-bit immediate (headline dZ -2.1 %: variants_r4_v23_ldsab.md)
     lds_char* dst = lds + isB * kStageBytes + buf * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
+    if constexpr (kTrCap) {
+      if (!isB && s.kk < tr_end) {  // a lower tile: rows of C_JI (see above)
+        // 32-bit scalar offset from the panel's tile (0, I) (the host checks the C buffer < 2 GiB)
+        const unsigned so = (unsigned)(s.kk >> 2) * (unsigned)p.A.row_tile_stride +
+                            (unsigned)(((s.kk & 3) * 64 + 8 * w) * (int)p.A.ld + 256 * h);
+        const auto trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(tr_base), 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void*)(dst + 8 * j * kKStepBytes), 16, a_tr_vo,
+                                                   so + (unsigned)(4 * j * (int)p.A.ld), 0, kGemmDmaAux);
+        s.advance(p.A);
+        return;
+      }
+    }
     // buffer_load ... lds from a scalar V# at the stream's K-step + the lane's 32-bit offset: no
     // 64-bit VALU address add per piece as global_load_lds needs (main loop 22 -> 14 VALU per
     // K-step and wave; headline dZ -2.9 %, forward -2.6 %: profiles/r4/variants_r4_v20_bufdma.md)
@@ -1059,6 +1104,32 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
           af[s][mi] = *(lds_frag*)src;
         }
       }
+    }
+  };
+  // A fragments of a transposed K-step (half C): two 4-row transposed reads per fragment. Untracked
+  // (asm) reads: the compiler's own wait for a tracked LDS read behind the in-flight LDS-DMA is a
+  // vmcnt(0) (it drained the operand prefetch every K-step); the K-step's counted lgkmcnt waits
+  // (a0_retire, lds_drain) retire them before their MFMAs.
+  auto read_a_tr = [&](auto buf_c, auto h_c, OP (&af)[NS][4]) {
+    if constexpr (kTrCap) {
+      constexpr int OFF0 = decltype(buf_c)::value * (kTile * kKStepBytes) + decltype(h_c)::value * kHalfBytes;
+      const unsigned base = (unsigned)(uintptr_t)lds + rd_tr;
+      auto one = [&](auto s_c, auto mi_c) {
+        constexpr int sv = decltype(s_c)::value, mv = decltype(mi_c)::value;
+        constexpr int off = OFF0 + 8 * sv * 1024 + 256 * mv;
+        u32x2 lo, hi;
+        asm volatile("ds_read_b64_tr_b16 %0, %2 offset:%c3\n\tds_read_b64_tr_b16 %1, %2 offset:%c4"
+                     : "=&v"(lo), "=&v"(hi)
+                     : "v"(base), "i"(off), "i"(off + 1024)
+                     : "memory");
+        af[sv][mv] = __builtin_bit_cast(OP, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      };
+      typedef std::integral_constant<int, 0> J0;
+      typedef std::integral_constant<int, 1> J1;
+      typedef std::integral_constant<int, 2> J2;
+      typedef std::integral_constant<int, 3> J3;
+      one(J0{}, J0{}); one(J0{}, J1{}); one(J0{}, J2{}); one(J0{}, J3{});
+      one(J1{}, J0{}); one(J1{}, J1{}); one(J1{}, J2{}); one(J1{}, J3{});
     }
   };
   auto read_b = [&](int buf, int h, OP (&bf)[NS][2]) {
@@ -1201,6 +1272,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   auto prologue = [&](int tile, int kb, int ke, int slot) {
     const int4 tt = sload_int4(p.tiles, tile);
     if (p.inv_a) stage_inv(tt.x, tt.y, slot);
+    if constexpr (kTrCap) {
+      tr_base = p.A.base + (long long)tt.x * p.A.kblk_stride;
+      tr_end = p.c_half ? 4 * tt.x : 0;  // K-steps of the lower tiles J < I (4 per tile)
+    }
     const int ns = ke - kb;
     const char* Ab = p.A.base + (long long)tt.x * p.A.row_tile_stride;
     const char* Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
@@ -1279,9 +1354,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if constexpr (MODE == kModeDz && !kF8)
     hpre = p.ndh != nullptr && (p.nh_dt == 1 || p.nh_dt == 2) && stile < 0 && nsteps == nk && nsteps >= 4 &&
            (nsteps & 1) == 0 && p.R % kTile == 0 && p.nd % kTile == 0;
-  auto kstep = [&](const int ks, auto cur_c, auto tail_c) {
+  auto kstep = [&](const int ks, auto cur_c, auto tail_c, auto tr_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
     constexpr int TAIL = decltype(tail_c)::value;
+    constexpr bool TR = decltype(tr_c)::value != 0;  // A of this K-step staged transposed (half C)
     if constexpr (kStreamMode) {
       // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
       if (cont && ks == nsteps - 2) {
@@ -1293,13 +1369,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
       if (cont && ks == nsteps - 1) sa1.init(na, 0, p.A, nk);
     }
     dma_wait(); barrier();          // phase 1 L (wait covers B1(t) for phase 2)
-    read_a(cur, 0, af);             //   operand reads first: their latency hides under the
+    if constexpr (TR) read_a_tr(cur_c, kI0, af);
+    else read_a(cur, 0, af);        //   operand reads first: their latency hides under the
     __builtin_amdgcn_sched_barrier(0);  // pin: the 8 A0 reads precede the B0 reads (a0_retire)
     read_b(cur, 0, bf0);            //   DMA issue that follows (~100-200 cycles per piece)
     if constexpr (TAIL == 2) stage_h(3, mt, nt);
     else stage(0, 1, sa1, nxt);     //   A1 of step ks+1
     a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
     lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
+    if constexpr (TR) __builtin_amdgcn_sched_barrier(0);  // (asm A reads: no MFMA above the wait)
     mma_quadrant(kI0, kI0, af, bf0);
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
     read_b(cur, 1, bf1);
@@ -1308,10 +1386,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
     mma_quadrant(kI0, kI1, af, bf1);
     barrier();                      // phase 3 L
-    read_a(cur, 1, af);
+    if constexpr (TR) read_a_tr(cur_c, kI1, af);
+    else read_a(cur, 1, af);
     if constexpr (TAIL != 0) stage_h(TAIL == 1 ? 1 : 5, mt, nt);
     else stage(1, 0, sb0, cur);     //   B0 of step ks+2
     barrier(); lds_drain();         // phase 3 C (A1 is restaged two phases later)
+    if constexpr (TR) __builtin_amdgcn_sched_barrier(0);
     mma_quadrant(kI1, kI0, af, bf0);
     // phase 4 L (covers A0(t+1), B0(t+1) for the next phase 1; the last K-step of an h-prefetch
     // tail has none, and its wait would be the first to hold for the h pieces' memory latency)
@@ -1329,18 +1409,27 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   const std::integral_constant<int, 2> kI2{};
   int ks2 = 0;
   const int nmain = nsteps - (hpre ? 2 : 0);
+  if constexpr (kTrCap) {
+    // half C: the lower tiles' K-steps first (an even count: the host enables half C only when
+    // every item starts at an even K-step, dz_half_c_eligible; 4 K-steps per tile)
+    const int ntr = tr_end > kb ? (tr_end < ke ? tr_end : ke) - kb : 0;
+    for (; ks2 + 1 < ntr; ks2 += 2) {
+      kstep(ks2, kI0, kI0, kI1);
+      kstep(ks2 + 1, kI1, kI0, kI1);
+    }
+  }
   for (; ks2 + 1 < nmain; ks2 += 2) {
-    kstep(ks2, kI0, kI0);
-    kstep(ks2 + 1, kI1, kI0);
+    kstep(ks2, kI0, kI0, kI0);
+    kstep(ks2 + 1, kI1, kI0, kI0);
   }
   if constexpr (MODE == kModeDz && !kF8) {
     if (hpre) {
-      kstep(ks2, kI0, kI1);
-      kstep(ks2 + 1, kI1, kI2);
+      kstep(ks2, kI0, kI1, kI0);
+      kstep(ks2 + 1, kI1, kI2, kI0);
       ks2 += 2;
     }
   }
-  if (ks2 < nsteps) kstep(ks2, kI0, kI0);
+  if (ks2 < nsteps) kstep(ks2, kI0, kI0, kI0);
   if (grp == 0) barrier();  // re-align the groups
   tmark(item, 2);
   // dZ, h prefetched: this thread's row statistics for the epilogue, loaded before the drain
@@ -1716,6 +1805,31 @@ constexpr int kUpLds = kSubStages * kSubStage + 4 * 64 * 8 + 64;  // ring + colu
 // piece merges cost more than the shorter K loop saves: profiles/r5/gemm_timing/diag_up.md)
 template <int KS> constexpr int diag_ksd() { return KS / 2 > 1 ? KS / 2 : 1; }
 template <int KS> constexpr int diag_up_blocks() { return 4 * diag_ksd<KS>() + 6 * KS; }
+// The LSE launch folded into the diagonal remainder (LseFold::on; launch_fwd_stats decides). When
+// the remainder is the diagonal tiles of exactly the second half of the rows (panels [n/256, rt):
+// the headline's 16 of 32), every partial of the first-half rows i and all but the diagonal
+// tile's partial of the second-half rows j = i + n are complete before the launch. So, per 64-row
+// group G of the remainder (rows j = n + 64 G ..): a side wave pre-merges those (lse_fold_pre),
+// the region block that completes the group's diagonal partial merges it (the 4th contributor),
+// and whichever of the two arrives second at the group's ticket finishes the 64 pairs with one
+// wave (lse_fold_finish: lse2 and the positive coefficient as lse_block, the loss into the LSE
+// launch's 64-bit fixed-point ticket, one arrival per group). Neither waits for the other, and
+// the LSE launch and its boundary go away.
+struct LseFold {
+  int on;
+  int n;                      // pairs (rows / 2)
+  int ngroups;                // 64-row groups of the remainder (loss-ticket arrivals)
+  const float* ypos;          // [n] positive logits (log2 units)
+  float* lse2;                // [Rpad] (world 1)
+  float* cpos;                // [Rpad]
+  unsigned long long* ticket; // the LSE scratch's loss ticket (zero; self-cleaning)
+  float* loss;                // mean loss
+  float2* pre;                // [Rpad] pre-merged (max, sum) states (rows i complete, rows j w/o the diagonal)
+  int* gcnt;                  // [ngroups] pre / diagonal arrival tickets (zero; self-cleaning)
+  float loss_scale;
+  double loss_fx;
+};
+
 // Side job of the launch: blocks [nup, gridDim.x) run side(block, count, smem) instead (the LDS is
 // this kernel's one array). The remainder waits on load latency with one 4-wave block per CU, so a
 // bandwidth-bound job (the raw forward's Z^T, DiagSideZt) runs beside it instead of in a later launch.
@@ -1723,9 +1837,83 @@ struct NoSide {
   int nup;
   __device__ void operator()(int, int, char*) const {}
 };
+// The 64 pairs of group G finished by one wave (lane = pair): the pre-merged states of rows i and
+// j, the diagonal tile's partial (m, s) of row j, then as lse_block.
+__device__ __forceinline__ void lse_fold_finish(const LseFold& lf, int G, float2 pi_, float2 pj, float m, float s) {
+  const int lane = threadIdx.x & 63;
+  const int i = 64 * G + lane, j = i + lf.n;
+  float mj = pj.x, sj = pj.y;
+  lse_merge(mj, sj, m, s);
+  const float yp = lf.ypos[i];
+  float l_i, l_j, a_i, a_j;
+  const float L2i = finish_row(pi_.x, pi_.y, yp, l_i, a_i), L2j = finish_row(mj, sj, yp, l_j, a_j);
+  lf.lse2[i] = L2i;
+  lf.lse2[j] = L2j;
+  lf.cpos[i] = -(a_i + a_j);
+  lf.cpos[j] = -(a_i + a_j);
+  const float tot = wave_sum(l_i + l_j);  // fixed tree: deterministic
+  if (lane == 0) {  // the LSE launch's ticket (lse_block): arrival, non-finite count, fixed-point sum
+    const bool fin = tot >= 0.f && tot < 3.0e38f;
+    const unsigned long long qv = fin ? (unsigned long long)llrint((double)tot * lf.loss_fx) : 0ull;
+    const unsigned long long add = (qv << 24) | (fin ? 1ull : (1ull << 12) | 1ull);
+    const unsigned long long old = __hip_atomic_fetch_add(lf.ticket, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((int)(old & 0xFFF) == lf.ngroups - 1) {
+      __hip_atomic_store(lf.ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long all = old + add;
+      lf.loss[0] = ((all >> 12) & 0xFFF) ? __builtin_nanf("") : (float)((double)(all >> 24) / lf.loss_fx * (double)lf.loss_scale);
+    }
+  }
+}
+
+// Group G's arrival ticket (lane 0 of the calling wave; agent scope, after the caller's
+// write-through stores drained): true for the second of the two arrivals, which resets it.
+__device__ __forceinline__ bool lse_fold_ticket(const LseFold& lf, int G) {
+  int last = 0;
+  if ((threadIdx.x & 63) == 0) {
+    const int old = __hip_atomic_fetch_add(lf.gcnt + G, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == 1;
+    if (last) __hip_atomic_store(lf.gcnt + G, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __builtin_amdgcn_readfirstlane(last) != 0;
+}
+
+// Side wave of group G: pre-merge rows i (all column tiles) and j (all but the diagonal tile nt),
+// publish them write-through, take the ticket; the second arrival finishes the group.
+__device__ __forceinline__ void lse_fold_pre(const SimParams& p, const LseFold& lf, int G) {
+  const int lane = threadIdx.x & 63;
+  const int i = 64 * G + lane, j = i + lf.n;
+  const int nt = j / kTile;  // the remainder's diagonal tile of row j's panel (world 1)
+  const int Tc = p.col_tiles, Rpad = p.Rpad;
+  float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
+  for (int t0 = 0; t0 < Tc; t0 += 8) {  // 8 column tiles per round, all 16 loads first
+    float2 vi[8], vj[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u < Tc ? t0 + u : t0;
+      vi[u] = p.part[(long long)t * Rpad + i];
+      vj[u] = p.part[(long long)t * Rpad + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (t0 + u < Tc) {
+        lse_merge(mi, si, vi[u].x, vi[u].y);
+        if (t0 + u != nt) lse_merge(mj, sj, vj[u].x, vj[u].y);
+      }
+  }
+  const auto prs = __builtin_amdgcn_make_buffer_rsrc(lf.pre, 0, 0x7FFFFFFF, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mi), __float_as_uint(si)}, prs, i * 8, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mj), __float_as_uint(sj)}, prs, j * 8, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!lse_fold_ticket(lf, G)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc(p.part + (long long)nt * Rpad, 0, 0x7FFFFFFF, 0x00020000);
+  const u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(drs, j * 8, 0, 16);
+  lse_fold_finish(lf, G, make_float2(mi, si), make_float2(mj, sj), __uint_as_float(d[0]), __uint_as_float(d[1]));
+}
+
 template <typename T, int FX, int KS>
 __device__ __forceinline__ void diag_up_region(const SimParams& p, float2* __restrict__ scratch, const int nup,
-                                               const int vb, char* smem) {
+                                               const int vb, char* smem, const LseFold& lf) {
 #if NTXENT_TIMING
   auto dmark = [&](int k) {
     if (threadIdx.x == 0) p.tstamp[(long long)vb * kTimingItems * kTimingMarks + k] = __builtin_amdgcn_s_memtime();
@@ -1965,16 +2153,33 @@ __device__ __forceinline__ void diag_up_region(const SimParams& p, float2* __res
   dmark(6);
   const int k = tid >> 6;  // wave 0 merges group a, wave 1 group b
   if (k > 1 || !((lastm >> k) & 1)) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
-  const int g = k == 0 ? a : b;
-  const auto srs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + g) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
-  u32x2 qv[4];
+  {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    const int g = k == 0 ? a : b;
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(scratch + (size_t)(tile * 4 + g) * 4 * 64, 0, 4 * 64 * 8, 0x00020000);
+    u32x2 qv[4];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) qv[kk] = __builtin_amdgcn_raw_buffer_load_b64(srs, (kk * 64 + lane) * 8, 0, 16);
-  float m = __uint_as_float(qv[0][0]), sm = __uint_as_float(qv[0][1]);
+    for (int kk = 0; kk < 4; ++kk) qv[kk] = __builtin_amdgcn_raw_buffer_load_b64(srs, (kk * 64 + lane) * 8, 0, 16);
+    float m = __uint_as_float(qv[0][0]), sm = __uint_as_float(qv[0][1]);
 #pragma unroll
-  for (int kk = 1; kk < 4; ++kk) lse_merge(m, sm, __uint_as_float(qv[kk][0]), __uint_as_float(qv[kk][1]));
-  p.part[(long long)nt * p.Rpad + r0 + 64 * g + lane] = make_float2(m, sm);
+    for (int kk = 1; kk < 4; ++kk) lse_merge(m, sm, __uint_as_float(qv[kk][0]), __uint_as_float(qv[kk][1]));
+    if (!lf.on) {
+      p.part[(long long)nt * p.Rpad + r0 + 64 * g + lane] = make_float2(m, sm);
+      return;
+    }
+    // LseFold: publish the diagonal partial write-through, then group G's ticket (lse_fold_pre)
+    const auto prs = __builtin_amdgcn_make_buffer_rsrc(p.part + (long long)nt * p.Rpad, 0, 0x7FFFFFFF, 0x00020000);
+    const int j = r0 + 64 * g + lane, G = (r0 + 64 * g - lf.n) >> 6;
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(m), __float_as_uint(sm)}, prs, j * 8, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!lse_fold_ticket(lf, G)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const auto qrs = __builtin_amdgcn_make_buffer_rsrc(lf.pre, 0, 0x7FFFFFFF, 0x00020000);
+    const u32x2 ui = __builtin_amdgcn_raw_buffer_load_b64(qrs, (j - lf.n) * 8, 0, 16);
+    const u32x2 uj = __builtin_amdgcn_raw_buffer_load_b64(qrs, j * 8, 0, 16);
+    lse_fold_finish(lf, G, make_float2(__uint_as_float(ui[0]), __uint_as_float(ui[1])),
+                    make_float2(__uint_as_float(uj[0]), __uint_as_float(uj[1])), m, sm);
+  }
 }
 
 // nupg: blocks of the grid that run regions (the first nupg; the rest run the side job). Normally
@@ -1983,14 +2188,21 @@ __device__ __forceinline__ void diag_up_region(const SimParams& p, float2* __res
 // region's block never waits on another one (arrival tickets only), so any nupg >= 1 completes.
 template <typename T, int FX, int KS, typename SIDE = NoSide>
 __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2* __restrict__ scratch, const SIDE side,
-                                                      const int nupg) {
+                                                      const int nupg, const LseFold lf) {
   __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   if ((int)blockIdx.x >= nupg) {
-    side((int)blockIdx.x - nupg, (int)gridDim.x - nupg, smem);
+    const int sb = (int)blockIdx.x - nupg;
+    // LseFold: side waves pre-merge the remainder's row groups first (4 groups per side block)
+    if (lf.on && 4 * sb < lf.ngroups) {
+      const int G = 4 * sb + (threadIdx.x >> 6);
+      if (G < lf.ngroups) lse_fold_pre(p, lf, G);
+      __syncthreads();
+    }
+    side(sb, (int)gridDim.x - nupg, smem);
     return;
   }
   for (int vb = (int)blockIdx.x; vb < side.nup; vb += nupg) {
-    diag_up_region<T, FX, KS>(p, scratch, side.nup, vb, smem);
+    diag_up_region<T, FX, KS>(p, scratch, side.nup, vb, smem, lf);
     __syncthreads();  // the next region restages the ring and the exchange area
   }
 }

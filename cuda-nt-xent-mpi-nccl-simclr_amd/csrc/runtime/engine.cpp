@@ -93,6 +93,8 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&one_, 4},
       // symmetric mode, fp32 plans: the received contributions follow the own slab (one stack)
       {(void**)&slabs_, Rp * g_.dim_n * 4 * (symm_ && ccs_ == 4 ? 1 + inc_.size() : 1)},
+      {(void**)&fold_pre_, world_ == 1 ? Rp * sizeof(float2) : 0},
+      {(void**)&fold_cnt_, world_ == 1 ? (Rp / 64 + 1) * sizeof(int) : 0},
       {(void**)&part_x_, symm_ ? (size_t)g_.col_tiles * Rp * sizeof(float2) : 0},
       {(void**)&xsend_, symm_ ? sym_xpack_floats2(jobs_, g_.row_tiles) * sizeof(float2) : 0},
       {(void**)&xrecv_, symm_ ? sym_xpack_floats2(inc_, g_.row_tiles) * sizeof(float2) : 0},
@@ -164,6 +166,14 @@ void Engine::forward(const void* h, hipStream_t s) {
   rr.inv = inv_;
   rr.zqt = zqt_local;
   rr.zt = bwd_;
+  // the LSE launch's outputs: the diagonal remainder's launch may compute them (rr.lse_folded)
+  rr.ypos = ypos_;
+  rr.lse2 = lse2_all_;
+  rr.cpos = cpos_;
+  rr.block_loss = block_loss_;
+  rr.loss = loss_;
+  rr.fold_pre = fold_pre_;
+  rr.fold_cnt = fold_cnt_;
   // forward GEMM operand: the e4m3 rows for fp8 plans, else zq itself (or the input rows: raw)
   char* op_all = f8_ ? zq8_all_ : zq_all_;
   const size_t op_bytes = f8_ ? Rp * g_.ld_k8 : Rp * g_.ld_k * cs_;
@@ -213,9 +223,9 @@ void Engine::forward(const void* h, hipStream_t s) {
     launch_fwd_stats(cfg_.compute, op_local, op_all, fwd_tiles_ + n_own_, n_fwd_ - n_own_, part_,
                      sbuf_ ? sbuf_ + (size_t)n_own_ * kTileElems * cs_ : nullptr, ws_ovl, g_, s);
   }
-  {
+  fault_point("lse");
+  if (!(raw && rr.lse_folded)) {
     NTXENT_TRACE("ntxent.lse");
-    fault_point("lse");
     if (q8_) {
       Q8Stats q8;
       q8.mneg2 = q8_mneg_;
@@ -256,11 +266,14 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
                      small_scratch_, g_, s, std::min(cfg_.small_splits, small_rows_pad(g_) / 64));
     return;
   }
+  // half C: upper coefficient tiles only, the dZ reads the lower ones transposed
+  const bool half_c = cfg_.keep_cos && !q8_ && half_c_enabled() && dz_half_c_eligible(bwd_, g_, n_dz_, ws_);
   {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");
     if (cfg_.keep_cos)
-      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr, dotp_, q8_ ? &q8 : nullptr);
+      launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr, dotp_, q8_ ? &q8 : nullptr,
+                  half_c);
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
@@ -284,7 +297,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
         q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
                         fuse_ ? &nf : nullptr, &q8, cpos_)
             : launch_dz(bwd_, cbuf_, zqt_all_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/bwd_ != DType::F32,
-                        fuse_ ? &nf : nullptr);
+                        fuse_ ? &nf : nullptr, nullptr, nullptr, half_c);
     if (fused) return;  // dh written by the dZ epilogue
   }
   {

@@ -296,14 +296,14 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
 
 // Kept cosines (compact, one slot per forward tile) -> coefficient buffer (all tiles).
 at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
-                float* dotp = nullptr) {
+                float* dotp = nullptr, bool half_c = false) {
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf), nullptr,
-              dotp);
+              dotp, nullptr, half_c);
   return cbuf;
 }
 
@@ -320,7 +320,7 @@ at::Tensor coef_gemm(const at::Tensor& zq_local, const at::Tensor& zq_all, const
 }
 
 at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P, const NormFuse* nf = nullptr,
-              bool* fused = nullptr) {
+              bool* fused = nullptr, bool half_c = false) {
   check_input(sc, "sc");
   check_input(zqt_all, "zqt_all");
   NTXENT_CHECK(zqt_all.numel() == (long)P.g.world * P.g.dim_n * P.g.ld_t, "zqt_all must be [world, dim_n, ld_t]");
@@ -331,7 +331,7 @@ at::Tensor dz(const at::Tensor& sc, const at::Tensor& zqt_all, const Plan& P, co
   auto ws = gemm_ws(sc, P.n_dz, P);
   const bool f = launch_dz(P.bwd(), sc.data_ptr(), zqt_all.data_ptr(),
                            reinterpret_cast<const int4*>(P.dz_tiles.data_ptr<int>()), P.n_dz, slabs.data_ptr(), ws, P.g,
-                           cur_stream(sc), f16, nf);
+                           cur_stream(sc), f16, nf, nullptr, nullptr, half_c);
   if (fused) *fused = f;
   return slabs;
 }
@@ -636,16 +636,26 @@ std::vector<at::Tensor> fused_forward(const at::Tensor& h, double T, const std::
     auto part = at::empty({P->g.col_tiles, P->g.rows_pad, 2}, opts(h, at::kFloat));
     auto sc = at::empty({(long)P->n_fwd * kTileElems}, opts(h, to_scalar(P->bwd())));
     auto ws = gemm_ws(h, P->n_fwd, *P);
-    const bool zt_fwd = launch_fwd_stats(P->comp, nullptr, nullptr, reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd,
-                     reinterpret_cast<float2*>(part.data_ptr<float>()), sc.data_ptr(), ws, P->g, s, BlockView{}, nullptr,
-                     P->n_fwd == P->n_own ? own_diag_tail(P->g) : 0, nullptr, &raw);
     auto lse2 = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
     auto cpos = at::empty({P->g.rows_pad}, opts(h, at::kFloat));
     auto block_loss = device_scratch(h, (size_t)lse_scratch_floats(P->g) * 4, 1);
     auto loss = at::empty({}, opts(h, at::kFloat));
-    launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(), lse2.data_ptr<float>(),
-               cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()), loss.data_ptr<float>(), P->g, s,
-               P->bwd(), nullptr, zt_fwd ? nullptr : zqt.data_ptr(), nullptr, zt_fwd ? nullptr : &raw);
+    // the LSE outputs: the diagonal remainder's launch may compute them itself (RawRows::lse_folded)
+    raw.ypos = ypos.data_ptr<float>();
+    raw.lse2 = lse2.data_ptr<float>();
+    raw.cpos = cpos.data_ptr<float>();
+    raw.block_loss = static_cast<float*>(block_loss.data_ptr());
+    raw.loss = loss.data_ptr<float>();
+    auto fold_pre = at::empty({P->g.rows_pad, 2}, opts(h, at::kFloat));
+    raw.fold_pre = reinterpret_cast<float2*>(fold_pre.data_ptr<float>());
+    raw.fold_cnt = static_cast<int*>(device_scratch(h, (size_t)(P->g.rows_pad / 64 + 1) * 4, 3).data_ptr());
+    const bool zt_fwd = launch_fwd_stats(P->comp, nullptr, nullptr, reinterpret_cast<const int4*>(P->fwd_tiles.data_ptr<int>()), P->n_fwd,
+                     reinterpret_cast<float2*>(part.data_ptr<float>()), sc.data_ptr(), ws, P->g, s, BlockView{}, nullptr,
+                     P->n_fwd == P->n_own ? own_diag_tail(P->g) : 0, nullptr, &raw);
+    if (!raw.lse_folded)
+      launch_lse(reinterpret_cast<const float2*>(part.data_ptr<float>()), ypos.data_ptr<float>(), lse2.data_ptr<float>(),
+                 cpos.data_ptr<float>(), static_cast<float*>(block_loss.data_ptr()), loss.data_ptr<float>(), P->g, s,
+                 P->bwd(), nullptr, zt_fwd ? nullptr : zqt.data_ptr(), nullptr, zt_fwd ? nullptr : &raw);
     return {loss, at::empty({0}, opts(h, to_scalar(P->bwd()))), zqt, inv, lse2, sc, cpos};
   }
   auto pr = prep(h, *P, c10::nullopt, c10::nullopt);
@@ -750,8 +760,11 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   }
   float* dp = fuse ? dotp.data_ptr<float>() : nullptr;
   at::Tensor cb;
+  // half C: upper coefficient tiles only, the dZ reads the lower ones transposed (whole-tile dZ)
+  const bool half_c = sc_in.has_value() && sc_in->defined() && half_c_enabled() &&
+                      dz_half_c_eligible(P->bwd(), P->g, P->n_dz, gemm_ws(h, P->n_dz, *P));
   if (sc_in.has_value() && sc_in->defined()) {
-    cb = coef(*sc_in, lse2, cpos, *P, dp);
+    cb = coef(*sc_in, lse2, cpos, *P, dp, half_c);
   } else {
     // (a raw-operand forward returns no unit rows: a second backward rebuilds them to recompute S)
     const at::Tensor zr = zq.numel() > 0 ? zq : prep(h, *P, c10::nullopt, c10::nullopt)[0];
@@ -771,7 +784,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
     nf.dh = dh.data_ptr();
   }
   bool fused = false;
-  auto slabs = dz(cb, zqt, *P, fuse ? &nf : nullptr, &fused);
+  auto slabs = dz(cb, zqt, *P, fuse ? &nf : nullptr, &fused, half_c);
   return fused ? dh : norm_bwd(slabs, h, inv, grad_out, *P);
 }
 
@@ -1127,6 +1140,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
   m.def("set_raw_forward", &ntxent::set_raw_forward, py::arg("on"));
   m.def("raw_forward_enabled", &ntxent::raw_forward_enabled);
+  m.def("set_lse_fold", &ntxent::set_lse_fold, py::arg("on"));
+  m.def("lse_fold_enabled", &ntxent::lse_fold_enabled);
+  m.def("set_half_c", &ntxent::set_half_c, py::arg("on"));
+  m.def("half_c_enabled", &ntxent::half_c_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));

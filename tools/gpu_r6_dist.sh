@@ -11,7 +11,7 @@ export TMPDIR=/tmp NTXENT_GPU_CHECK=1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r6dist}; mkdir -p $OUT
 SEL=${2:-"tests/test_gpu_multiproc.py -k rccl"}
 NS=${3:-"2 8"}
-timeout -k 10 900 python -u -m pytest $SEL -v -rA --durations 10 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
+eval timeout -k 10 900 python -u -m pytest $SEL -v -rA --durations 10 --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1
 rc=$?
 grep -E "passed|failed" $OUT/pytest.log | tail -2
 grep -E "^(FAILED|ERROR)" $OUT/pytest.log | head -30
