@@ -1534,7 +1534,7 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
             zs.tx = g.rows_pad / 64;
             zs.ntiles = zs.tx * (g.dim_n / 64);  // (rows [dim, dim_n) of Z^T: zeros)
             const int nside = std::min(zs.ntiles, NTXENT_ZT_SIDE_PER_CU * ws.num_cus);
-            if (4 * nside < lf.ngroups) lf.on = 0;  // (every group needs its pre-merging side wave)
+            if (nside < lf.ngroups) lf.on = 0;  // (every group needs its pre-merging side block)
             launch_up(zs, nside);
             side_zt = true;
           }

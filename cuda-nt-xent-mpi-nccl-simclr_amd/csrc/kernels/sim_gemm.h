@@ -1877,28 +1877,41 @@ __device__ __forceinline__ bool lse_fold_ticket(const LseFold& lf, int G) {
   return __builtin_amdgcn_readfirstlane(last) != 0;
 }
 
-// Side wave of group G: pre-merge rows i (all column tiles) and j (all but the diagonal tile nt),
-// publish them write-through, take the ticket; the second arrival finishes the group.
-__device__ __forceinline__ void lse_fold_pre(const SimParams& p, const LseFold& lf, int G) {
-  const int lane = threadIdx.x & 63;
+// Side block of group G (4 waves, lane = pair): wave w pre-merges column tiles [Tc w / 4, Tc (w + 1)
+// / 4) of rows i (all) and j (all but the diagonal tile nt), one round of loads each; wave 0 merges
+// the four states in wave order, publishes them write-through and takes the ticket; the second
+// arrival finishes the group.
+__device__ __forceinline__ void lse_fold_pre(const SimParams& p, const LseFold& lf, int G, char* smem) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = 64 * G + lane, j = i + lf.n;
   const int nt = j / kTile;  // the remainder's diagonal tile of row j's panel (world 1)
   const int Tc = p.col_tiles, Rpad = p.Rpad;
+  const int t0 = Tc * w / 4, t1 = Tc * (w + 1) / 4;
   float mi = kNegInf, si = 0.f, mj = kNegInf, sj = 0.f;
-  for (int t0 = 0; t0 < Tc; t0 += 8) {  // 8 column tiles per round, all 16 loads first
+  for (int tb = t0; tb < t1; tb += 8) {  // (8 tiles: Tc <= 32 is one round)
     float2 vi[8], vj[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int t = t0 + u < Tc ? t0 + u : t0;
+      const int t = tb + u < t1 ? tb + u : tb;
       vi[u] = p.part[(long long)t * Rpad + i];
       vj[u] = p.part[(long long)t * Rpad + j];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (t0 + u < Tc) {
+      if (tb + u < t1) {
         lse_merge(mi, si, vi[u].x, vi[u].y);
-        if (t0 + u != nt) lse_merge(mj, sj, vj[u].x, vj[u].y);
+        if (tb + u != nt) lse_merge(mj, sj, vj[u].x, vj[u].y);
       }
+  }
+  float4* xs = reinterpret_cast<float4*>(smem);  // [4 waves][64 pairs] (mi, si, mj, sj)
+  xs[w * 64 + lane] = make_float4(mi, si, mj, sj);
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int ww = 1; ww < 4; ++ww) {
+    const float4 v = xs[ww * 64 + lane];
+    lse_merge(mi, si, v.x, v.y);
+    lse_merge(mj, sj, v.z, v.w);
   }
   const auto prs = __builtin_amdgcn_make_buffer_rsrc(lf.pre, 0, 0x7FFFFFFF, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(mi), __float_as_uint(si)}, prs, i * 8, 0, 16);
@@ -2192,10 +2205,9 @@ __global__ __launch_bounds__(256) void diag_up_kernel(const SimParams p, float2*
   __shared__ __attribute__((aligned(16))) char smem[kUpLds];  // one array: a second __shared__ object drains the LDS-DMA
   if ((int)blockIdx.x >= nupg) {
     const int sb = (int)blockIdx.x - nupg;
-    // LseFold: side waves pre-merge the remainder's row groups first (4 groups per side block)
-    if (lf.on && 4 * sb < lf.ngroups) {
-      const int G = 4 * sb + (threadIdx.x >> 6);
-      if (G < lf.ngroups) lse_fold_pre(p, lf, G);
+    // LseFold: the first ngroups side blocks pre-merge one remainder row group each, first
+    if (lf.on && sb < lf.ngroups) {
+      lse_fold_pre(p, lf, sb, smem);
       __syncthreads();
     }
     side(sb, (int)gridDim.x - nupg, smem);
