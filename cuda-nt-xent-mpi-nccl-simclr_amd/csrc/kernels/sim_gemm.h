@@ -406,8 +406,17 @@ __device__ __forceinline__ void coef_epilogue(f32x4 (&acc)[NMI][4], const int (&
       u32x4 v;
 #pragma unroll
       for (int k = 0; k < 4; ++k) v[k] = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)u[k]);
-      *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(slot) +
-                                ctile_off(row_base + c0 + (lane >> 2), col_base + (blk / RB) * 32 + 8 * (lane & 3), 2)) = v;
+      char* cdst = reinterpret_cast<char*>(slot) +
+                   ctile_off(row_base + c0 + (lane >> 2), col_base + (blk / RB) * 32 + 8 * (lane & 3), 2);
+#ifndef NTXENT_COEF_STORE
+#define NTXENT_COEF_STORE 0  // A/B switch: 0 default policy, 1 non-temporal, 2 write-through
+#endif
+      if constexpr (NTXENT_COEF_STORE == 1)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(cdst));
+      else if constexpr (NTXENT_COEF_STORE == 2)
+        store16_wt(slot, cdst - reinterpret_cast<char*>(slot), v);
+      else
+        *reinterpret_cast<u32x4*>(cdst) = v;
     }
   }
 }
@@ -1835,6 +1844,7 @@ struct LseFold {
 // bandwidth-bound job (the raw forward's Z^T, DiagSideZt) runs beside it instead of in a later launch.
 struct NoSide {
   int nup;
+  static constexpr int kLds = 16;  // LDS bytes the side job needs (see sk_reduce_kernel)
   __device__ void operator()(int, int, char*) const {}
 };
 // The 64 pairs of group G finished by one wave (lane = pair): the pre-merged states of rows i and
@@ -2239,10 +2249,21 @@ __device__ __forceinline__ int sk_frag_off(int row, int col) {  // float offset 
   return (((4 * wa + wb) * 32 + 4 * mi + ni) * 64 + lane) * 4 + (row & 3);
 }
 
-template <typename TS, int FX>
-__global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float2* __restrict__ colp) {
+// SIDE: blocks [nred, gridDim.x) run side(block, count, smem) instead (the split-K forward's Z^T of
+// the raw-operand rows, DiagSideZt, beside the slab-latency-bound reduce: config 4 writes 32 MiB
+// of Z^T there instead of in the LSE launch).
+template <typename TS, int FX, typename SIDE = NoSide>
+__global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float2* __restrict__ colp, const int nred = 0,
+                                                        const SIDE side = SIDE{}) {
   __shared__ float red[4][16][2];
   __shared__ int last_flag;
+  if constexpr (!std::is_same<SIDE, NoSide>::value) {
+    __shared__ __attribute__((aligned(16))) char sm[SIDE::kLds];
+    if ((int)blockIdx.x >= nred) {
+      side((int)blockIdx.x - nred, (int)gridDim.x - nred, sm);
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tile = blockIdx.x >> 4, strip = blockIdx.x & 15;
   const int4 t = p.tiles[tile];
