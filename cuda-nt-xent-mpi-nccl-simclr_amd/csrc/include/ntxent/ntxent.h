@@ -227,9 +227,6 @@ struct RawRows {
   mutable bool lse_folded = false;
 };
 void set_lse_fold(bool on);  // default: NTXENT_LSE_FOLD (unset: on)
-// split-K forward (raw rows): Z^T written beside the split-K reduce instead of by the LSE launch
-void set_sk_zt_side(bool on);  // default: NTXENT_SK_ZT (unset: on)
-bool sk_zt_side_enabled();
 bool lse_fold_enabled();
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp);  // world 1, 2-byte in & comp, rows % 256, dim % 64
 void set_raw_forward(bool on);  // default on (off: the zq path, for A/B and tests)

@@ -459,10 +459,9 @@ struct DiagSideZt {
   T* zqt;
   const float* inv;
   int dk, ldt, tx, ntiles;
-  static constexpr int kLds = 64 * (64 + 16 / (int)sizeof(T)) * (int)sizeof(T);
   __device__ void operator()(int b, int nb, char* smem) const {
     typedef T Tile[64][64 + 16 / sizeof(T)];
-    static_assert(sizeof(Tile) <= kUpLds && sizeof(Tile) == kLds, "Z^T side job: tile exceeds the remainder's LDS");
+    static_assert(sizeof(Tile) <= kUpLds, "Z^T side job: tile exceeds the remainder's LDS");
     Tile& tile = *reinterpret_cast<Tile*>(smem);
     for (int t = b; t < ntiles; t += nb) {
       transpose_tile<T, Ts>(h, zqt, dk, dk, ldt, t % tx, t / tx, tile, inv);
@@ -1306,12 +1305,7 @@ static std::atomic<bool> g_lse_fold{[] {
   return e == nullptr || std::string(e) != "0";
 }()};
 void set_lse_fold(bool on) { g_lse_fold = on; }
-static std::atomic<bool> g_sk_zt{[] {
-  const char* e = std::getenv("NTXENT_SK_ZT");
-  return e == nullptr || std::string(e) != "0";
-}()};
-void set_sk_zt_side(bool on) { g_sk_zt = on; }
-bool sk_zt_side_enabled() { return g_sk_zt.load(); }
+
 bool lse_fold_enabled() { return g_lse_fold.load(); }
 static double lse_loss_fx(const Geometry& g, int nb);
 
@@ -1459,37 +1453,10 @@ bool launch_fwd_stats(DType comp, const void* zq_local, const void* zq_all, cons
       using TS = typename dev::StoreT<Tc>::type;
       float2* colp = reinterpret_cast<float2*>(static_cast<char*>(ws.ptr) + sk_counter_bytes(ws.num_cus) +
                                                (size_t)2 * ws.num_cus * kTileElems * sizeof(float));
-      bool side_zt = false;
-      if constexpr (sizeof(TS) == 2 && !std::is_same<Tc, dev::fp8e4m3>::value) {
-        if (raw && raw->zqt && sk_zt_side_enabled()) {
-          // Z^T = (h inv)^T beside the reduce (its blocks wait on slab loads; the transpose is
-          // bandwidth-bound), instead of in the LSE launch
-          using Ts = typename std::conditional<std::is_same<Tc, dev::bf16r>::value, __bf16, Tc>::type;
-          NTXENT_CHECK(raw->zt == (std::is_same<TS, __bf16>::value ? DType::BF16 : DType::F16) && g.dim_n % 64 == 0,
-                       "fwd_stats: Z^T dtype must be the plan's backward dtype");
-          dev::DiagSideZt<TS, Ts> zs;
-          zs.nup = 0;
-          zs.h = static_cast<const Ts*>(raw->h);
-          zs.zqt = static_cast<TS*>(raw->zqt);
-          zs.inv = raw->inv;
-          zs.dk = g.dim;
-          zs.ldt = (int)g.ld_t;
-          zs.tx = g.rows_pad / 64;
-          zs.ntiles = zs.tx * (g.dim_n / 64);
-          const int nside = std::min(zs.ntiles, NTXENT_ZT_SIDE_PER_CU * ws.num_cus);
-          const dim3 sg(ntiles * 16 + nside);
-          if (p.fixed_shift)
-            hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 1, decltype(zs)>), sg, dim3(256), 0, stream, p, colp, ntiles * 16, zs);
-          else
-            hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 0, decltype(zs)>), sg, dim3(256), 0, stream, p, colp, ntiles * 16, zs);
-          side_zt = true;
-          zt_done = true;
-        }
-      }
-      if (!side_zt) {
-        if (p.fixed_shift) hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 1>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp, 0, dev::NoSide{});
-        else hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 0>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp, 0, dev::NoSide{});
-      }
+      // (Z^T of the raw rows beside this reduce as side blocks: config 4 forward +3.5 us, the
+      // reduce slowed by more than the LSE launch's transpose costs: profiles/r6/README.md)
+      if (p.fixed_shift) hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 1>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp);
+      else hipLaunchKernelGGL((dev::sk_reduce_kernel<TS, 0>), dim3(ntiles * 16), dim3(256), 0, stream, p, colp);
     }
     if (main_done) NTXENT_HIP_CHECK(hipEventRecord(main_done, stream));
     if constexpr (!std::is_same<Tc, dev::fp8e4m3>::value) {

@@ -1844,7 +1844,6 @@ struct LseFold {
 // bandwidth-bound job (the raw forward's Z^T, DiagSideZt) runs beside it instead of in a later launch.
 struct NoSide {
   int nup;
-  static constexpr int kLds = 16;  // LDS bytes the side job needs (see sk_reduce_kernel)
   __device__ void operator()(int, int, char*) const {}
 };
 // The 64 pairs of group G finished by one wave (lane = pair): the pre-merged states of rows i and
@@ -2249,21 +2248,10 @@ __device__ __forceinline__ int sk_frag_off(int row, int col) {  // float offset 
   return (((4 * wa + wb) * 32 + 4 * mi + ni) * 64 + lane) * 4 + (row & 3);
 }
 
-// SIDE: blocks [nred, gridDim.x) run side(block, count, smem) instead (the split-K forward's Z^T of
-// the raw-operand rows, DiagSideZt, beside the slab-latency-bound reduce: config 4 writes 32 MiB
-// of Z^T there instead of in the LSE launch).
-template <typename TS, int FX, typename SIDE = NoSide>
-__global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float2* __restrict__ colp, const int nred = 0,
-                                                        const SIDE side = SIDE{}) {
+template <typename TS, int FX>
+__global__ __launch_bounds__(256) void sk_reduce_kernel(const SimParams p, float2* __restrict__ colp) {
   __shared__ float red[4][16][2];
   __shared__ int last_flag;
-  if constexpr (!std::is_same<SIDE, NoSide>::value) {
-    __shared__ __attribute__((aligned(16))) char sm[SIDE::kLds];
-    if ((int)blockIdx.x >= nred) {
-      side((int)blockIdx.x - nred, (int)gridDim.x - nred, sm);
-      return;
-    }
-  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tile = blockIdx.x >> 4, strip = blockIdx.x & 15;
   const int4 t = p.tiles[tile];

@@ -1140,8 +1140,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_fp8_backward", &ntxent::set_fp8_backward, py::arg("on"));
   m.def("set_raw_forward", &ntxent::set_raw_forward, py::arg("on"));
   m.def("raw_forward_enabled", &ntxent::raw_forward_enabled);
-  m.def("set_sk_zt_side", &ntxent::set_sk_zt_side, py::arg("on"));
-  m.def("sk_zt_side_enabled", &ntxent::sk_zt_side_enabled);
   m.def("set_lse_fold", &ntxent::set_lse_fold, py::arg("on"));
   m.def("lse_fold_enabled", &ntxent::lse_fold_enabled);
   m.def("set_half_c", &ntxent::set_half_c, py::arg("on"));

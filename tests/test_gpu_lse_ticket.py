@@ -97,9 +97,9 @@ def test_ticket_loss_low_loss_low_tau(ext, rows, dim):
 @pytest.mark.parametrize("raw", [True, False])
 def test_zt_exact_against_unit_rows(ext, raw, rows, dim):
     # Z^T (the dZ GEMM's B operand) element-wise: the raw-operand forward's side job (DiagSideZt,
-    # beside the diagonal remainder at 8192 x 2048, beside the split-K reduce at 2048 x 8192)
-    # writes fp16((h * inv)^T) from the returned inv; the unit-row forward's LSE-launch transpose
-    # writes zq^T. Exact, padded rows/columns zero.
+    # beside the diagonal remainder at 8192 x 2048) or the LSE launch's raw transpose (split-K
+    # forward at 2048 x 8192) writes fp16((h * inv)^T) from the returned inv; the unit-row
+    # forward's LSE-launch transpose writes zq^T. Exact, padded rows/columns zero.
     h = _views(rows, dim, seed=5)
     old = ext.raw_forward_enabled()
     try:
