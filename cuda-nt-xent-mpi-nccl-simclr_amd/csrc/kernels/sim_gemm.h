@@ -179,6 +179,18 @@ struct KStream {
       if (kin == o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }
     }
   }
+  // half C: a K-step staged from the transposed tile advances the position only (ptr was placed
+  // at the item's first regular K-step by seek)
+  __device__ __forceinline__ void skip() {
+    if (left > 0) {
+      --left;
+      ++kk;
+    }
+  }
+  __device__ __forceinline__ void seek(const char* base, long long k0, const OperandDesc& o) {
+    kin = (int)(k0 % o.kblk);
+    ptr = base + (k0 / o.kblk) * o.kblk_stride + kin;
+  }
 };
 
 // C^T staging of one 64x64 region by one wave (coef_kernel): LDS row L (C column L) is 128 B of
@@ -1011,12 +1023,15 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     asm volatile("" : "+v"(a_tr_vo), "+v"(rd_tr));
   }
   // stage half-tile h of operand A (isB = 0) or B (isB = 1) for the stream's K-step into buf
-  auto stage = [&](int isB, int h, KStream& s, int buf) {
+  // trm (half C, operand A): 0 the staged K-step is a regular one (a regular K-step only stages
+  // K-steps past the item's lower tiles), 2 a lower tile's (a half-C K-step two or more steps
+  // before the last one), 1 either: tested (the prologue and the last two half-C K-steps)
+  auto stage = [&](int isB, int h, KStream& s, int buf, int trm = 1) {
     // LDS layout [A even | A odd | B even | B odd] (32 KiB each): every operand read of either
     // parity is its lane base + a 16-bit immediate (headline dZ -2.1 %: variants_r4_v23_ldsab.md)
     lds_char* dst = lds + isB * kStageBytes + buf * (kTile * kKStepBytes) + (128 * h + 16 * w) * kKStepBytes;
     if constexpr (kTrCap) {
-      if (!isB && s.kk < tr_end) {  // a lower tile: rows of C_JI (see above)
+      if (!isB && (trm == 2 || (trm == 1 && s.kk < tr_end))) {  // a lower tile: rows of C_JI (see above)
         // 32-bit scalar offset from the panel's tile (0, I) (the host checks the C buffer < 2 GiB)
         const unsigned so = (unsigned)(s.kk >> 2) * (unsigned)p.A.row_tile_stride +
                             (unsigned)(((s.kk & 3) * 64 + 8 * w) * (int)p.A.ld + 256 * h);
@@ -1025,7 +1040,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
         for (int j = 0; j < 2; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(trs, (lds_void*)(dst + 8 * j * kKStepBytes), 16, a_tr_vo,
                                                    so + (unsigned)(4 * j * (int)p.A.ld), 0, kGemmDmaAux);
-        s.advance(p.A);
+        s.skip();
         return;
       }
     }
@@ -1290,6 +1305,12 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     const char* Bb = p.B.base + (long long)(tt.y - p.b_tile0) * p.B.row_tile_stride;
     const long long k0 = (long long)kb * kKStepBytes;
     sa0.init(Ab, k0, p.A, ns); sa1.init(Ab, k0, p.A, ns);
+    if constexpr (kTrCap) {
+      if (tr_end > kb) {  // half C: the regular K-steps start at tr_end (the lower ones use tr_base)
+        sa0.seek(Ab, (long long)tr_end * kKStepBytes, p.A);
+        sa1.seek(Ab, (long long)tr_end * kKStepBytes, p.A);
+      }
+    }
     sb0.init(Bb, k0, p.B, ns); sb1.init(Bb, k0, p.B, ns);
     if constexpr (kF8 && MODE != kModeDz) {
       // fp8: thread t fetches the dword whose low byte is the E8M0 scale of A row t (t < 256) or
@@ -1366,7 +1387,10 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   auto kstep = [&](const int ks, auto cur_c, auto tail_c, auto tr_c) {
     constexpr int cur = decltype(cur_c)::value, nxt = cur ^ 1;
     constexpr int TAIL = decltype(tail_c)::value;
-    constexpr bool TR = decltype(tr_c)::value != 0;  // A of this K-step staged transposed (half C)
+    // A of this K-step staged transposed (half C); 2: one of the last two such K-steps (its A
+    // stages may be regular ones)
+    constexpr bool TR = decltype(tr_c)::value != 0;
+    constexpr int TRM = decltype(tr_c)::value == 0 ? 0 : (decltype(tr_c)::value == 2 ? 1 : 2);
     if constexpr (kStreamMode) {
       // hand-over: A0, B0, B1 of K-step ks + 2 and A1 of ks + 1 are the next item's K-step 0
       if (cont && ks == nsteps - 2) {
@@ -1383,7 +1407,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     __builtin_amdgcn_sched_barrier(0);  // pin: the 8 A0 reads precede the B0 reads (a0_retire)
     read_b(cur, 0, bf0);            //   DMA issue that follows (~100-200 cycles per piece)
     if constexpr (TAIL == 2) stage_h(3, mt, nt);
-    else stage(0, 1, sa1, nxt);     //   A1 of step ks+1
+    else stage(0, 1, sa1, nxt, TRM);  // A1 of step ks+1
     a0_retire(); barrier();         // phase 1 C: A0 is restaged next phase -> its 8 reads retire
     lds_drain();                    //   before the barrier; the 4 B0 reads may retire after it
     if constexpr (TR) __builtin_amdgcn_sched_barrier(0);  // (asm A reads: no MFMA above the wait)
@@ -1391,7 +1415,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     dma_wait(); barrier();          // phase 2 L (covers A1(t) for phase 3)
     read_b(cur, 1, bf1);
     if constexpr (TAIL != 0) stage_h(TAIL == 1 ? 0 : 4, mt, nt);
-    else stage(0, 0, sa0, cur);     //   A0 of step ks+2
+    else stage(0, 0, sa0, cur, TRM);  // A0 of step ks+2
     barrier(); lds_drain();         // phase 2 C (B1 is restaged two phases later)
     mma_quadrant(kI0, kI1, af, bf1);
     barrier();                      // phase 3 L
@@ -1422,9 +1446,14 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
     // half C: the lower tiles' K-steps first (an even count: the host enables half C only when
     // every item starts at an even K-step, dz_half_c_eligible; 4 K-steps per tile)
     const int ntr = tr_end > kb ? (tr_end < ke ? tr_end : ke) - kb : 0;
-    for (; ks2 + 1 < ntr; ks2 += 2) {
+    for (; ks2 + 3 < ntr; ks2 += 2) {  // their stages are all lower-tile K-steps
       kstep(ks2, kI0, kI0, kI1);
       kstep(ks2 + 1, kI1, kI0, kI1);
+    }
+    if (ks2 + 1 < ntr) {  // the last two: their stages cross into the regular K-steps
+      kstep(ks2, kI0, kI0, kI2);
+      kstep(ks2 + 1, kI1, kI0, kI2);
+      ks2 += 2;
     }
   }
   for (; ks2 + 1 < nmain; ks2 += 2) {
