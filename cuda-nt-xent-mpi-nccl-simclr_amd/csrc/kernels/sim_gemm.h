@@ -176,7 +176,7 @@ struct KStream {
       ++kk;
       ptr += kKStepBytes;
       kin += kKStepBytes;
-      if (kin == o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }
+      if (kin == (int)o.kblk) { kin = 0; ptr += o.kblk_stride - o.kblk; }  // (K blocks < 2 GiB: 32-bit test)
     }
   }
   // half C: a K-step staged from the transposed tile advances the position only (ptr was placed
