@@ -112,7 +112,6 @@ class Engine {
   bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
   float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
   float* dot_ = nullptr;       // dot [Rpad]
-  int* dot_cnt_ = nullptr;     // folded dot reduce's counters (launch_coef dot_cnt)
   // symmetric data-parallel mode (Negatives::kSymmetric, engine_sym.cpp)
   bool symm_ = false;
   std::vector<SymJob> jobs_, inc_;

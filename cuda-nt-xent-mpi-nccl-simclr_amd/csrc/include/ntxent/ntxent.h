@@ -227,8 +227,6 @@ struct RawRows {
   mutable bool lse_folded = false;
 };
 void set_lse_fold(bool on);  // default: NTXENT_LSE_FOLD (unset: on)
-void set_dot_fold(bool on);  // default: NTXENT_DOT_FOLD (unset: on): launch_coef's dot_out in-launch
-bool dot_fold_enabled();
 bool lse_fold_enabled();
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp);  // world 1, 2-byte in & comp, rows % 256, dim % 64
 void set_raw_forward(bool on);  // default on (off: the zq path, for A/B and tests)
@@ -306,10 +304,7 @@ int dot_slots(const Geometry& g);
 // the partials of the dequantised coefficients (plus the exact positive term).
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf = nullptr, float* dotp = nullptr, const Q8Stats* q8 = nullptr, bool half_c = false,
-                 float* dot_out = nullptr, int* dot_cnt = nullptr);
-// dot_out (with dotp; 16-bit, mirrored layout): also dot[Rpad] = the row sums of dotp, by side blocks
-// of the same launch (no launch_dot_reduce); dot_cnt: 2 zeroed ints (self-cleaning).
+                 void* mbuf = nullptr, float* dotp = nullptr, const Q8Stats* q8 = nullptr, bool half_c = false);
 // half_c: write only the upper coefficient tiles (an off-diagonal tile's mirror is skipped; the
 // dZ launched with half_c reads C_IJ, J < I, as C_JI^T). Only with dz_half_c_eligible.
 // dot[Rpad] = row sums of dotp.

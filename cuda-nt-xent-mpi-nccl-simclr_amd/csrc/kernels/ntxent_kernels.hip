@@ -1305,12 +1305,6 @@ static std::atomic<bool> g_lse_fold{[] {
   return e == nullptr || std::string(e) != "0";
 }()};
 void set_lse_fold(bool on) { g_lse_fold = on; }
-static std::atomic<bool> g_dot_fold{[] {
-  const char* e = std::getenv("NTXENT_DOT_FOLD");
-  return e == nullptr || std::string(e) != "0";
-}()};
-void set_dot_fold(bool on) { g_dot_fold = on; }
-bool dot_fold_enabled() { return g_dot_fold.load(); }
 
 bool lse_fold_enabled() { return g_lse_fold.load(); }
 static double lse_loss_fx(const Geometry& g, int nb);
@@ -1656,7 +1650,7 @@ void launch_lse(const float2* part, const float* ypos, float* lse2_all, float* c
 
 void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all, const float* cpos,
                  const int4* tiles, int ntiles, const Geometry& g, hipStream_t stream,
-                 void* mbuf, float* dotp, const Q8Stats* q8, bool half_c, float* dot_out, int* dot_cnt) {
+                 void* mbuf, float* dotp, const Q8Stats* q8, bool half_c) {
   if (ntiles == 0) return;
   dev::SimParams p = base_params(g);
   NTXENT_CHECK(!half_c || (mbuf == nullptr && q8 == nullptr && g.world == 1 && (comp == DType::F16 || comp == DType::BF16)),
@@ -1682,20 +1676,10 @@ void launch_coef(DType comp, const void* sbuf, void* cbuf, const float* lse2_all
     NTXENT_HIP_CHECK(hipGetLastError());
     return;
   }
-  int nside = 0;
-  if (dot_out && dotp && dot_fold_enabled()) {  // the dot reduce as side blocks of this launch
-    NTXENT_CHECK(dot_cnt != nullptr && mbuf == nullptr, "coef: folded dot reduce needs its counters, mirrored layout");
-    nside = (g.rows_pad + 7) / 8;
-    p.dfold_main = 16 * ntiles;
-    p.dfold_side = nside;
-    p.dfold_dot = dot_out;
-    p.dfold_cnt = dot_cnt;
-  }
   dispatch_comp(comp, [&](auto tc) {
     using Tc = decltype(tc);
-    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(16 * ntiles + nside), dim3(64), 0, stream, p);
+    hipLaunchKernelGGL((dev::coef_kernel<Tc>), dim3(16 * ntiles), dim3(64), 0, stream, p);
   });
-  if (dot_out && nside == 0 && dotp) launch_dot_reduce(dotp, dot_out, g, stream);
   NTXENT_HIP_CHECK(hipGetLastError());
 }
 

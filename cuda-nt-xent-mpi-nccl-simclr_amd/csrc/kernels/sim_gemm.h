@@ -97,14 +97,6 @@ struct SimParams {
   // as the transpose of C_JI (dz_tr_stage / ds_read_b64_tr_b16): 64 MiB fewer C bytes written at
   // the headline
   int c_half;
-  // dot reduce folded into the coefficient launch (coef_kernel; launch_coef with dot_out): the
-  // first dfold_main blocks are the coefficient waves, each counting itself done in dfold_cnt[0]
-  // after its dot partials (write-through) drained; the dfold_side blocks after them (dispatched
-  // after every coefficient block) wait for the count, sum 8 rows' slots each into dfold_dot, and
-  // the last of them resets both counters (dfold_cnt[1]: side arrivals)
-  int dfold_main, dfold_side;
-  float* dfold_dot;
-  int* dfold_cnt;
   // raw-operand forward (RawRows): A / B are the input rows h, not unit rows; the accumulators are
   // normalised by inv_a[A row] * inv_b[B row] before the epilogue (null: unit-row operands)
   const float* inv_a;
@@ -218,10 +210,7 @@ __device__ __forceinline__ int ct_swz(int L) {
 // that reduction into this launch -- each 64-row group's last contributing wave sums its slots,
 // found by an agent-scope ticket -- measured 42 -> 64 us for the pass at the headline: every
 // wave waits for its ticket's return under contention. profiles/r5/coef_dot/.)
-// (write-through: a folded dot reduce in the same launch reads them after a counted arrival)
-__device__ __forceinline__ void dot_slot_store(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ void dot_slot_store(float* p, float v) { *p = v; }
 
 // Tile index of coefficient tile (mt, nt) in cbuf (row-major [row_tiles][c_ld] tiles).
 __device__ __forceinline__ long long ctile_index(const SimParams& p, int mt, int nt) {
@@ -1773,70 +1762,11 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 // (canonical fragment order: 16 fragments of 512 B) -> C into the coefficient buffer. 9 KiB of
 // LDS per wave keeps many independent waves in flight per CU (the pass is HBM-bound), and 16
 // waves per tile keep a small problem's few tiles (36 at B = 1024/view) spread over the chip.
-// Folded dot reduce (SimParams::dfold_*), one side block = one wave = 8 rows x 8 slot groups.
-// Every coefficient block was dispatched before any side block (in-order dispatch), so the count
-// it waits for is reached by blocks that are running or done.
-__device__ __forceinline__ void dot_fold_side(const SimParams& p, int sb, int nside) {
-  const int lane = threadIdx.x;
-  // (bounded: ~2 s at most, so a wrong count can never hold the GPU; the dot is then garbage and
-  // the gradient tests fail instead)
-  if (lane == 0)
-    for (int it = 0; it < (1 << 23) &&
-                     __hip_atomic_load(p.dfold_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.dfold_main;
-         ++it)
-      __builtin_amdgcn_s_sleep(4);
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the wait
-  const int r = 8 * sb + (lane >> 3), g = lane & 7;
-  const int nslot = 4 * p.col_tiles;
-  float s = 0.f;
-  if (r < p.Rpad) {
-    const auto drs = __builtin_amdgcn_make_buffer_rsrc(p.dotp, 0, 0x7FFFFFFF, 0x00020000);
-    int k = g;
-    for (; k + 120 < nslot; k += 128) {  // 16 loads in flight (headline: 128 slots = one round)
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(drs, (int)(((long long)(k + 8 * u) * p.Rpad + r) * 4), 0, 16));
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    for (; k < nslot; k += 8)
-      s += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(drs, (int)(((long long)k * p.Rpad + r) * 4), 0, 16));
-  }
-  s += __shfl_xor(s, 1);  // fixed tree: deterministic
-  s += __shfl_xor(s, 2);
-  s += __shfl_xor(s, 4);
-  if (g == 0 && r < p.Rpad) p.dfold_dot[r] = s;
-  if (lane == 0) {
-    const int old = __hip_atomic_fetch_add(p.dfold_cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == nside - 1) {  // every side block is past its wait: reset for the next launch
-      __hip_atomic_store(p.dfold_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(p.dfold_cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <typename T, bool Q8 = false> __device__ __forceinline__ void coef_region(const SimParams& p, char* smem);
-
 template <typename T, bool Q8 = false>
 __global__ __launch_bounds__(64) void coef_kernel(const SimParams p) {
   __shared__ __attribute__((aligned(16))) char smem[Q8 ? 2 * 64 * 80 : (sizeof(T) == 2 ? kCoefWaveLds : 16)];
-  if (p.dfold_main > 0 && (int)blockIdx.x >= p.dfold_main) {
-    dot_fold_side(p, (int)blockIdx.x - p.dfold_main, (int)gridDim.x - p.dfold_main);
-    return;
-  }
-  coef_region<T, Q8>(p, smem);
-  if (p.dfold_main > 0) {  // this wave's dot partials (write-through) drained: count it done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(p.dfold_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-template <typename T, bool Q8>
-__device__ __forceinline__ void coef_region(const SimParams& p, char* smem) {
   const int lane = threadIdx.x;
-  const int idx = xcd_remap(blockIdx.x, p.dfold_main > 0 ? p.dfold_main : (int)gridDim.x);
+  const int idx = xcd_remap(blockIdx.x, gridDim.x);
   const int tidx = idx >> 4, w = (idx >> 1) & 7, half = idx & 1;
   const int wm = w >> 2, wn = w & 3;
   const int4 t = p.tiles[tidx];

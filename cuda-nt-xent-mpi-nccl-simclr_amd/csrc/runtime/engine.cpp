@@ -104,7 +104,6 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&dz_rows_, symm_ ? (size_t)4 * (world_ + 1) * g_.row_tiles * (g_.dim_n / kTile) * sizeof(int4) : 0},
       {(void**)&dotp_, fuse_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
       {(void**)&dot_, fuse_ ? Rp * 4 : 0},
-      {(void**)&dot_cnt_, fuse_ ? 2 * sizeof(int) : 0},
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
       {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
       {&ws_.ptr, ws_.bytes},
@@ -274,11 +273,11 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     fault_point("coef");
     if (cfg_.keep_cos)
       launch_coef(bwd_, sbuf_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, g_, s, nullptr, dotp_, q8_ ? &q8 : nullptr,
-                  half_c, fuse_ ? dot_ : nullptr, fuse_ ? dot_cnt_ : nullptr);  // (+ dot, in the same launch)
+                  half_c);
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
-    if (fuse_ && !cfg_.keep_cos) launch_dot_reduce(dotp_, dot_, g_, s);
+    if (fuse_) launch_dot_reduce(dotp_, dot_, g_, s);
   }
   if (zqt_pending_) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));

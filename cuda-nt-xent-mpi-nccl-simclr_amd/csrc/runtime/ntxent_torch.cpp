@@ -296,15 +296,14 @@ at::Tensor lse(const at::Tensor& part, const at::Tensor& ypos, at::Tensor& lse2_
 
 // Kept cosines (compact, one slot per forward tile) -> coefficient buffer (all tiles).
 at::Tensor coef(const at::Tensor& sbuf, const at::Tensor& lse2_all, const at::Tensor& cpos, const Plan& P,
-                float* dotp = nullptr, bool half_c = false, float* dot_out = nullptr) {
+                float* dotp = nullptr, bool half_c = false) {
   check_input(sbuf, "sbuf");
   NTXENT_CHECK(sbuf.numel() == (long)P.n_fwd * kTileElems, "sbuf does not match the plan's forward tiles");
   const at::DeviceGuard guard(sbuf.device());
   auto cbuf = at::empty({(long)P.g.row_tiles * P.g.col_tiles * kTileElems}, sbuf.options());
   launch_coef(P.bwd(), sbuf.data_ptr(), cbuf.data_ptr(), lse2_all.data_ptr<float>(), cpos.data_ptr<float>(),
               reinterpret_cast<const int4*>(P.fwd_tiles.data_ptr<int>()), P.n_fwd, P.g, cur_stream(sbuf), nullptr,
-              dotp, nullptr, half_c, dot_out,
-              dot_out ? static_cast<int*>(device_scratch(sbuf, 8, 4).data_ptr()) : nullptr);
+              dotp, nullptr, half_c);
   return cbuf;
 }
 
@@ -765,7 +764,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   const bool half_c = sc_in.has_value() && sc_in->defined() && half_c_enabled() &&
                       dz_half_c_eligible(P->bwd(), P->g, P->n_dz, gemm_ws(h, P->n_dz, *P));
   if (sc_in.has_value() && sc_in->defined()) {
-    cb = coef(*sc_in, lse2, cpos, *P, dp, half_c, fuse ? dot.data_ptr<float>() : nullptr);  // (+ dot)
+    cb = coef(*sc_in, lse2, cpos, *P, dp, half_c);
   } else {
     // (a raw-operand forward returns no unit rows: a second backward rebuilds them to recompute S)
     const at::Tensor zr = zq.numel() > 0 ? zq : prep(h, *P, c10::nullopt, c10::nullopt)[0];
@@ -774,7 +773,7 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   at::Tensor dh, go;
   NormFuse nf;
   if (fuse) {
-    if (!(sc_in.has_value() && sc_in->defined())) launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
+    launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
     go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
     dh = at::empty_like(h);
     nf.h = h.data_ptr();
@@ -1142,8 +1141,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_raw_forward", &ntxent::set_raw_forward, py::arg("on"));
   m.def("raw_forward_enabled", &ntxent::raw_forward_enabled);
   m.def("set_lse_fold", &ntxent::set_lse_fold, py::arg("on"));
-  m.def("set_dot_fold", &ntxent::set_dot_fold, py::arg("on"));
-  m.def("dot_fold_enabled", &ntxent::dot_fold_enabled);
   m.def("lse_fold_enabled", &ntxent::lse_fold_enabled);
   m.def("set_half_c", &ntxent::set_half_c, py::arg("on"));
   m.def("half_c_enabled", &ntxent::half_c_enabled);

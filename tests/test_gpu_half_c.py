@@ -80,26 +80,3 @@ def test_half_c_engine_matches_full_c(ext):
         ext.set_half_c(old)
     assert outs[0][0] == outs[1][0]
     assert torch.equal(outs[0][1], outs[1][1])
-
-
-@pytest.mark.parametrize("rows,dim", [(8192, 2048), (8192, 512), (2048, 8192)])
-def test_dot_fold_matches_dot_launch(ext, rows, dim):
-    # the dot reduce as side blocks of the coefficient launch (SimParams::dfold_*) against the
-    # separate dot_reduce launch: the same sums in another fixed order (a bf16 ulp at most in dh),
-    # bitwise repeatable, within the usual tolerance of the fp64 oracle
-    h = _views(rows, dim, seed=dim + 1)
-    old = ext.dot_fold_enabled()
-    try:
-        ext.set_dot_fold(False)
-        _, g0 = _grad(h, 0.1)
-        ext.set_dot_fold(True)
-        _, g1 = _grad(h, 0.1)
-        _, g2 = _grad(h, 0.1)
-    finally:
-        ext.set_dot_fold(old)
-    assert torch.equal(g1, g2)
-    scale = g0.float().abs().max().item()
-    assert (g1.float() - g0.float()).abs().max().item() <= 1e-2 * scale
-    x = h.double().requires_grad_(True)
-    (gr,) = torch.autograd.grad(R.ntxent_loss(x, 0.1), x)
-    assert (g1.double() - gr).abs().max().item() <= 8e-3 * gr.abs().max().item()
