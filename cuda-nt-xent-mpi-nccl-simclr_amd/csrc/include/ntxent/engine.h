@@ -110,6 +110,7 @@ class Engine {
   size_t cs_ = 2;             // bytes per element of the backward dtype (zq, ZqT, cosines, C)
   bool f8_ = false;           // fp8 forward GEMM (e4m3 copy zq8_all_), fp16 backward
   bool fuse_ = false;          // normalisation backward in the dZ epilogue (NormFuse)
+  int* dot_cnt_ = nullptr;     // dot fold counters (NormFuse::dot_cnt)
   float* dotp_ = nullptr;      // dot partials [Rpad][dot_slots] (fuse_)
   float* dot_ = nullptr;       // dot [Rpad]
   // symmetric data-parallel mode (Negatives::kSymmetric, engine_sym.cpp)

@@ -324,9 +324,14 @@ void launch_coef_gemm(DType comp, const void* zq_local, const void* zq_all, void
 // computed per tile from the fp16-staged g, h, inv and dot; the dZ slab is not written. The
 // launchers return whether they fused (not for fp32 plans or d % 8 != 0: then the slab is
 // written and launch_norm_bwd runs).
-// dot: the reduced z_i . g_i (launch_dot_reduce). (Summing the coefficient pass's slots in the dZ
-// epilogue instead measured slower: dZ +4.6 / +6.3 / +10 us at the headline / config 4 / config 5
-// against the 5-6 us launch it removes, profiles/r5/variants_dotfold.)
+// dot: the reduced z_i . g_i (launch_dot_reduce). (Summing the coefficient pass's slots in every
+// dZ tile's epilogue measured slower: dZ +4.6 / +6.3 / +10 us at the headline / config 4 /
+// config 5 against the 5-6 us launch it removes, profiles/r5/variants_dotfold.)
+// dot_cnt (with dotp = the coefficient pass's slots; only where dz_dot_fold_eligible): the dZ grid
+// reduces dotp into dot itself instead, each block its 1/G share of the rows before its first
+// item, published through dot_cnt[0] (sc1 stores, one count per block); the epilogues read dot a
+// main loop later (split-K pieces: the reduce launch does). dot_cnt: 2 ints, zero before the
+// first use (self-cleaning).
 struct NormFuse {
   const void* h = nullptr;
   DType in = DType::BF16;
@@ -334,6 +339,8 @@ struct NormFuse {
   const float* dot = nullptr;
   const float* grad_out = nullptr;  // device scalar
   void* dh = nullptr;
+  const float* dotp = nullptr;      // dot fold: the slots
+  int* dot_cnt = nullptr;           // dot fold: counters (non-null: fold)
 };
 // comp = FP8 with q8: the fp8 backward's dZ (cbuf = e4m3 C tiles, zqt_all = Q8Stats::zq8t;
 // block-scaled MFMA, per-row dequantisation and the exact positive term in the epilogue).
@@ -349,6 +356,10 @@ bool launch_dz(DType comp, const void* cbuf, const void* zqt_all, const int4* ti
 bool dz_half_c_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace& ws);
 void set_half_c(bool on);  // default: NTXENT_HALF_C (unset: on)
 bool half_c_enabled();
+// NormFuse::dot_cnt allowed: a 16-bit fused dZ, fold enabled.
+bool dz_dot_fold_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace& ws);
+void set_dot_fold(bool on);  // default: NTXENT_DOT_FOLD (unset: on)
+bool dot_fold_enabled();
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first

@@ -796,19 +796,8 @@ __global__ __launch_bounds__(256) void dot_reduce_kernel(const float* __restrict
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = blockIdx.x * 32 + (lane & 31), sg = 2 * w + (lane >> 5);
   __shared__ float part[8][32];
-  float s = 0.f;
-  if (i < rows) {
-    int k = sg;
-    for (; k + 120 < nslot; k += 128) {  // 16 loads in flight
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = dotp[(long long)(k + 8 * u) * rows + i];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    for (; k < nslot; k += 8) s += dotp[(long long)k * rows + i];
-  }
-  part[sg][lane & 31] = s;
+  // (the same arithmetic as the dZ's folded form, dz_dot_fold: bitwise the same dot)
+  part[sg][lane & 31] = i < rows ? dot_slot_sum(dotp, nslot, rows, i, sg) : 0.f;
   __syncthreads();
   if (threadIdx.x < 32 && blockIdx.x * 32 + (int)threadIdx.x < rows) {
     float t = 0.f;
@@ -1329,6 +1318,18 @@ bool dz_half_c_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorks
   if (pieces > 0) return ((nk + pieces - 1) / pieces) % 2 == 0;
   return make_schedule(n_dz, nk, cus).sk_tiles == 0;
 }
+static std::atomic<bool> g_dot_fold{[] {
+  const char* e = std::getenv("NTXENT_DOT_FOLD");
+  return e == nullptr || std::string(e) != "0";
+}()};
+void set_dot_fold(bool on) { g_dot_fold = on; }
+bool dot_fold_enabled() { return g_dot_fold.load(); }
+// The dot reduce folds into a 16-bit fused dZ (whole / stream-K tiles: published to its own
+// epilogues; split-K pieces: to the reduce launch); callers then skip launch_dot_reduce
+// (NormFuse::dot_cnt).
+bool dz_dot_fold_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace&) {
+  return (comp == DType::F16 || comp == DType::BF16) && n_dz > 0 && g.dim % 8 == 0 && dot_fold_enabled();
+}
 bool raw_forward_enabled() { return g_raw_fwd.load(); }
 bool raw_forward_eligible(const Geometry& g, DType in, DType comp) {
   // (fp16 rows on a bf16 plan would keep fp16 cosines for a bf16 backward: not offered)
@@ -1772,6 +1773,14 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
   p.c_half = half_c ? 1 : 0;
   const bool fused = comp != DType::F32 && apply_norm_fuse(p, nf, g);
   if (fused) NTXENT_CHECK(nf->dot != nullptr, "dz: fused normalisation backward without dot");
+  if (nf && nf->dot_cnt) {
+    // dot reduce folded in (dz_dot_fold): the grid sums nf->dotp into nf->dot itself
+    NTXENT_CHECK(fused && !f8 && nf->dotp && dz_dot_fold_eligible(comp, g, ntiles, ws),
+                 "dz: dot fold needs the fused 16-bit epilogue");
+    p.dotp = const_cast<float*>(nf->dotp);
+    p.dot_nslot = dot_slots(g);
+    p.dot_cnt = pieces == 0 ? nf->dot_cnt : nullptr;  // split-K: the reduce launch reads dot
+  }
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);
     launch_sim_gemm<Tc, dev::kModeDz>(grid, p, stream);

@@ -123,6 +123,9 @@ struct SimParams {
   int nh_dt, nd;
   const float* ninv;     // ... 1 / |h_i|
   const float* ndot;     // ... dot_i (reduced dotp)
+  int dot_nslot;         // ... > 0: the dZ grid reduces dotp (dot_nslot slots) into ndot itself
+  int* dot_cnt;          //     (dz_dot_fold), published through these [2] zeroed counters (self-
+                         //     cleaning) to its own epilogues; null for split-K pieces
   const float* ngo;      // ... grad_out (device scalar)
   float nalpha;          // ... 1 / (2N tau)
   void* ndh;             // ... output dh [R][nd] (non-null: fused epilogue)
@@ -756,6 +759,96 @@ __device__ __forceinline__ void dz8_finish(f32x4 (&acc)[8][4], const SimParams& 
   }
 }
 
+// Slot group sg (of 8) of dot_i = sum_k dotp[k][i]: slots sg, sg + 8, ... in increasing order, 16
+// loads in flight. dot_reduce_kernel sums the 8 groups in sg order; dz_dot_fold and dz_dot's
+// fallback use the same order, so every path gives dot_i bitwise.
+__device__ __forceinline__ float dot_slot_sum(const float* dotp, int nslot, int rows, int i, int sg) {
+  float s = 0.f;
+  int k = sg;
+  for (; k + 120 < nslot; k += 128) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = dotp[(long long)(k + 8 * u) * rows + i];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
+  }
+  for (; k < nslot; k += 8) s += dotp[(long long)k * rows + i];
+  return s;
+}
+
+// dZ with the dot reduce folded in (SimParams::dot_nslot; replaces the dot_reduce launch): every
+// block of the persistent grid, before its first item, sums dot_i for its share of rows (32-row
+// chunks, dot_reduce_kernel's arithmetic) and stores them sc1; one lane adds 1 to dot_cnt[0]
+// after a block barrier that follows every wave's retirement of those stores. The epilogue's
+// reads (dz_dot) come one whole main loop later. Split-K pieces (no
+// epilogue here: sk_dz_reduce_kernel reads dot after the kernel boundary) fold without the count.
+__device__ __forceinline__ void dz_dot_fold(const SimParams& p, lds_char* lds, int tid) {
+  typedef __attribute__((address_space(3))) float lds_fl;
+  lds_fl* part = (lds_fl*)lds;  // [2 halves][8 slot groups][32 rows]
+  const int G = gridDim.x, rows = p.Rpad;
+  const int rpb = ((rows + G - 1) / G + 31) & ~31;
+  const int r0 = blockIdx.x * rpb, r1 = r0 + rpb < rows ? r0 + rpb : rows;
+  const int hf = tid >> 8, lt = tid & 255, ln = lt & 63, sg = 2 * (lt >> 6) + (ln >> 5);
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.ndot), 0, 0x7FFFFFFF, 0x00020000);
+  for (int c0 = r0; c0 < r1; c0 += 64) {
+    const int i = c0 + 32 * hf + (ln & 31);
+    part[(hf * 8 + sg) * 32 + (ln & 31)] = i < r1 ? dot_slot_sum(p.dotp, p.dot_nslot, rows, i, sg) : 0.f;
+    __syncthreads();
+    if (lt < 32 && c0 + 32 * hf + lt < r1) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) t += part[(hf * 8 + g) * 32 + lt];
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), drs, (c0 + 32 * hf + lt) * 4, 0, 16);  // sc1
+    }
+    __syncthreads();
+  }
+  // (counted by the caller once the stores have retired: after the first item's prologue wait,
+  // or at the exit of a block without items, dz_dot_exit; split-K pieces are not counted: the
+  // reduce launch reads dot after the kernel boundary)
+}
+// dot_i for the dZ epilogue. With the fold, the calling wave first polls (once: `state` 0 -> 1)
+// until every block has counted; a poll that runs out (blocks not co-resident: never seen) makes
+// the wave sum the slots itself from then on (state 2), in the same order. sc1 loads (the
+// producer stored sc1: MI355X_MICROARCH.md, visibility, first table row).
+constexpr int kDotSpinBound = 1 << 14;  // x s_sleep 8 (~0.2 us): a few ms
+template <bool FOLD>
+__device__ __forceinline__ float dz_dot(const SimParams& p, int row, int& state) {
+  if (!FOLD || p.dot_cnt == nullptr) return p.ndot[row];
+  if (state == 0) {
+    int n = 0;
+    while (__hip_atomic_load(p.dot_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int)gridDim.x && n < kDotSpinBound) {
+      __builtin_amdgcn_s_sleep(8);
+      ++n;
+    }
+    state = n < kDotSpinBound ? 1 : 2;
+  }
+  if (state == 2) {  // (serial: dot_slot_sum's additions in the same order, few registers)
+    float t = 0.f;
+    for (int g = 0; g < 8; ++g) {
+      float s = 0.f;
+      for (int k = g; k < p.dot_nslot; k += 8) s += p.dotp[(long long)k * p.Rpad + row];
+      t += s;
+    }
+    return t;
+  }
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.ndot), 0, 0x7FFFFFFF, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(drs, row * 4, 0, 16));
+}
+// Kernel exit of a folding dZ: a block that had no item counts its fold now; the last block out
+// returns both counters to zero (every poll has ended: a block polls before it leaves).
+__device__ __forceinline__ void dz_dot_exit(const SimParams& p, int tid, bool counted) {
+  if (!counted) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fold's sc1 stores
+  __syncthreads();
+  if (tid == 0) {
+    if (!counted) __hip_atomic_fetch_add(p.dot_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(p.dot_cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (int)gridDim.x - 1) {
+      __hip_atomic_store(p.dot_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.dot_cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // h tile of the fused dZ epilogue prefetched into the ring (dz_store_h): 8 pieces of 128 rows x
 // 128 B (piece i = rows 128 (i & 1).., bytes 128 (i >> 1).. of the tile's 512-byte row segment,
 // the ring's chunk swizzle), DMA'd by the last two K-steps in place of their trailing (clamped)
@@ -823,8 +916,10 @@ __device__ __forceinline__ void dz_store_h(f32x4 (&acc)[8][4], const SimParams& 
 
 // dZ epilogue (swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r])
 // of output tile (mt, nt); `lds` (>= 128 KiB, free) stages the fp16 tile for coalesced rows.
+template <typename T>
 __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p, int mt, int nt, int tid,
-                                         const int (&rb)[8], const int (&cb)[4], lds_char* lds) {
+                                         const int (&rb)[8], const int (&cb)[4], lds_char* lds, int& dstate) {
+  constexpr bool kFold = !std::is_same<T, fp8e4m3>::value && sizeof(T) == 2;  // dz_dot_fold: 16-bit dZ
   typedef __attribute__((address_space(3))) u32x4 lds_u4;
   const int lane = tid & 63;
   // swapped orientation: lane holds out[m = rb + (lane&15)][n = cb + 4(lane>>4) + r]
@@ -840,7 +935,7 @@ __device__ __forceinline__ void dz_store(f32x4 (&acc)[8][4], const SimParams& p,
     float iv0 = 0.f, dt0 = 0.f;
     if (p.ndh && tid < kTile && mt * kTile + tid < p.R) {
       iv0 = p.ninv[mt * kTile + tid];
-      dt0 = p.ndot[mt * kTile + tid];
+      dt0 = dz_dot<kFold>(p, mt * kTile + tid, dstate);
     }
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
@@ -1328,6 +1423,16 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // prologue).
   const bool streaming = kStreamMode && p.sk_tiles == 0 && nk >= 2 && (nk & 1) == 0;
   bool streamed = false;  // this item's first two K-steps were staged by the previous item
+  int dstate = 0;         // dZ, dot fold: dz_dot's poll state
+  bool dot_counted = false;  // ... this block's fold counted (at its first item)
+  if constexpr (MODE == kModeDz && !kF8 && sizeof(T) == 2) {
+    // every block (one with no work too) folds its share of the dot reduce before its first item
+    // and counts it once its first prologue wait has retired the stores (dz_dot_signal); inside
+    // the item loop the fold put ~30 more SGPR spills around it, and a peeled first prologue
+    // (the fold under its DMA) put 4x the lane reads into the K-loop. The fold's LDS (2 KiB) is
+    // the epilogue's per-row coefficients.
+    if (p.dot_nslot > 0) dz_dot_fold(p, lds + kGemmLds, threadIdx.x);
+  }
   auto tmark = [&](int item, int k) {
 #if NTXENT_TIMING
     if (threadIdx.x == 0 && item < kTimingItems)
@@ -1364,6 +1469,13 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
 
   asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // A0(0), B0(0) retired
   barrier();
+  if constexpr (MODE == kModeDz && !kF8 && sizeof(T) == 2) {
+    // the fold's sc1 stores preceded this item's 14 DMA pieces: every wave's wait above retired
+    // them (in order), and the barrier follows every wave's wait
+    if (item == 0 && p.dot_cnt != nullptr && threadIdx.x == 0)
+      __hip_atomic_fetch_add(p.dot_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dot_counted = true;
+  }
   if constexpr (kF8 && MODE != kModeDz) {  // this item's scale bytes (landed with A0(0), B0(0))
     const int r16_ = lane & 15;
     unsigned av[8], bv[4];
@@ -1475,7 +1587,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if constexpr (MODE == kModeDz && !kF8) {
     if (hpre && threadIdx.x < kTile) {
       hiv = p.ninv[mt * kTile + threadIdx.x];
-      hdt = p.ndot[mt * kTile + threadIdx.x];
+      hdt = dz_dot<sizeof(T) == 2>(p, mt * kTile + threadIdx.x, dstate);
     }
   }
   if (kStreamMode && cont) {
@@ -1535,7 +1647,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   if constexpr (MODE == kModeDz) {
     if constexpr (kF8) dz8_finish(acc, p, mt, nt, rb, cb, lane);
     if (!kF8 && hpre) dz_store_h(acc, p, mt, nt, tid, rb, cb, lds, hiv, hdt);
-    else dz_store(acc, p, mt, nt, tid, rb, cb, lds);
+    else dz_store<T>(acc, p, mt, nt, tid, rb, cb, lds, dstate);
   } else if constexpr (MODE == kModeCoef) {
     coef_epilogue<typename StoreT<T>::type, 8>(acc, rb, cb, 0, 0, mt, nt, t.z, lds, p, lane);
   } else {
@@ -1756,6 +1868,9 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   // loop's barriers, so no barrier here)
   if constexpr (!kStreamMode) __syncthreads();
   }  // work items
+  if constexpr (MODE == kModeDz && !kF8 && sizeof(T) == 2) {
+    if (p.dot_cnt) dz_dot_exit(p, threadIdx.x, dot_counted);
+  }
 }
 
 // Store-mode coefficient pass: one wave per 64x64 region (wm, wn, half) of a kept cosine tile

@@ -104,6 +104,7 @@ Engine::Engine(const EngineConfig& cfg, Comm* comm) : cfg_(cfg), comm_(comm) {
       {(void**)&dz_rows_, symm_ ? (size_t)4 * (world_ + 1) * g_.row_tiles * (g_.dim_n / kTile) * sizeof(int4) : 0},
       {(void**)&dotp_, fuse_ ? Rp * (size_t)dot_slots(g_) * 4 : 0},
       {(void**)&dot_, fuse_ ? Rp * 4 : 0},
+      {(void**)&dot_cnt_, fuse_ ? 2 * sizeof(int) : 0},
       {(void**)&fwd_tiles_, ft.size() * sizeof(int4)},
       {(void**)&dz_tiles_, dt.size() * sizeof(int4)},
       {&ws_.ptr, ws_.bytes},
@@ -268,6 +269,8 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
   }
   // half C: upper coefficient tiles only, the dZ reads the lower ones transposed
   const bool half_c = cfg_.keep_cos && !q8_ && half_c_enabled() && dz_half_c_eligible(bwd_, g_, n_dz_, ws_);
+  // the dot reduce folded into the dZ (NormFuse::dot_cnt)
+  const bool dfold = fuse_ && !q8_ && dz_dot_fold_eligible(bwd_, g_, n_dz_, ws_);
   {
     NTXENT_TRACE("ntxent.coef");
     fault_point("coef");
@@ -277,7 +280,7 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     else
       launch_coef_gemm(cfg_.compute, zq_local, zq_all_, cbuf_, lse2_all_, cpos_, fwd_tiles_, n_fwd_, ws_, g_, s,
                        BlockView{}, dotp_);
-    if (fuse_) launch_dot_reduce(dotp_, dot_, g_, s);
+    if (fuse_ && !dfold) launch_dot_reduce(dotp_, dot_, g_, s);
   }
   if (zqt_pending_) {
     NTXENT_HIP_CHECK(hipStreamWaitEvent(s, ev_zqt_, 0));
@@ -293,6 +296,10 @@ void Engine::backward(const float* grad_out, void* dh, hipStream_t s) {
     nf.dot = dot_;
     nf.grad_out = grad_out ? grad_out : one_;
     nf.dh = dh;
+    if (dfold) {
+      nf.dotp = dotp_;
+      nf.dot_cnt = dot_cnt_;
+    }
     const bool fused =
         q8_ ? launch_dz(DType::FP8, cbuf_, zq8t_, dz_tiles_, n_dz_, slabs_, ws_, g_, s, /*out_f16=*/true,
                         fuse_ ? &nf : nullptr, &q8, cpos_)

@@ -772,8 +772,15 @@ at::Tensor fused_backward(const at::Tensor& h, const at::Tensor& zq, const c10::
   }
   at::Tensor dh, go;
   NormFuse nf;
+  // the dot reduce folded into the dZ (NormFuse::dot_cnt): per-stream counters (device_scratch)
+  const bool dfold = fuse && dz_dot_fold_eligible(P->bwd(), P->g, P->n_dz, gemm_ws(h, P->n_dz, *P));
   if (fuse) {
-    launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
+    if (dfold) {
+      nf.dotp = dp;
+      nf.dot_cnt = static_cast<int*>(device_scratch(h, 2 * sizeof(int), 4).data_ptr());
+    } else {
+      launch_dot_reduce(dp, dot.data_ptr<float>(), P->g, cur_stream(h));
+    }
     go = grad_out.to(at::kFloat).reshape({-1}).narrow(0, 0, 1).contiguous();
     dh = at::empty_like(h);
     nf.h = h.data_ptr();
@@ -1144,6 +1151,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lse_fold_enabled", &ntxent::lse_fold_enabled);
   m.def("set_half_c", &ntxent::set_half_c, py::arg("on"));
   m.def("half_c_enabled", &ntxent::half_c_enabled);
+  m.def("set_dot_fold", &ntxent::set_dot_fold, py::arg("on"));
+  m.def("dot_fold_enabled", &ntxent::dot_fold_enabled);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));
