@@ -6,7 +6,8 @@ block of the dZ's persistent grid sums its share of the rows before its first it
 them through a counter that the epilogues poll. Both use the same additions in the same order
 (dot_slot_sum), so the gradient must be BITWISE the unfolded one, at every shape: the headline,
 config 5 (16384 rows), config 4 (d = 8192), a padded row count (6000 rows: 192 dZ tiles on 256
-CUs, stream-K items), and config 2 (d = 512: split-K dZ pieces fold for the reduce launch). Repeated steps check that the counters clean themselves.
+CUs, stream-K items), and config 2 (d = 512: split-K dZ pieces fold for the reduce launch).
+Repeated steps check that the counters clean themselves.
 Reference intent: /root/reference/src/ntxent_kernel.cu:232-262 (the backward's gradient).
 """
 import pytest
