@@ -360,6 +360,8 @@ bool half_c_enabled();
 bool dz_dot_fold_eligible(DType comp, const Geometry& g, int n_dz, const GemmWorkspace& ws);
 void set_dot_fold(bool on);  // default: NTXENT_DOT_FOLD (unset: on)
 bool dot_fold_enabled();
+void set_dot_fold_spin(int polls);  // test hook: 0 forces the epilogues' fallback sum
+int dot_fold_spin();
 
 // Sub-block dZ GEMM (symmetric mode): out[rows of `tiles`] (+)= A * B over K = k_tiles * 256
 // columns, A = tile-blocked coefficients starting at `a` (the tile of row panel 0 and the first

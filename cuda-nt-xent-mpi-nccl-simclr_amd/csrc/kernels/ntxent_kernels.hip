@@ -1324,6 +1324,12 @@ static std::atomic<bool> g_dot_fold{[] {
 }()};
 void set_dot_fold(bool on) { g_dot_fold = on; }
 bool dot_fold_enabled() { return g_dot_fold.load(); }
+// polls (s_sleep 8 each, ~0.2 us) before an epilogue sums its rows' dot itself; the count is
+// complete a main loop before the first poll, so the bound only guards a grid whose blocks are not
+// all resident. Tests set 0: every epilogue takes the fallback (its result must not change).
+static std::atomic<int> g_dot_spin{1 << 14};
+void set_dot_fold_spin(int polls) { g_dot_spin = polls < 0 ? 0 : polls; }
+int dot_fold_spin() { return g_dot_spin.load(); }
 // The dot reduce folds into a 16-bit fused dZ (whole / stream-K tiles: published to its own
 // epilogues; split-K pieces: to the reduce launch); callers then skip launch_dot_reduce
 // (NormFuse::dot_cnt).
@@ -1780,6 +1786,7 @@ bool launch_dz(DType comp, const void* sc, const void* zqt_all, const int4* tile
     p.dotp = const_cast<float*>(nf->dotp);
     p.dot_nslot = dot_slots(g);
     p.dot_cnt = pieces == 0 ? nf->dot_cnt : nullptr;  // split-K: the reduce launch reads dot
+    p.dot_spin = dot_fold_spin();
   }
   dispatch_gemm(comp, [&](auto tc) {
     using Tc = decltype(tc);

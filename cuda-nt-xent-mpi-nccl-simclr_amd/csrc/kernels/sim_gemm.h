@@ -124,6 +124,7 @@ struct SimParams {
   const float* ninv;     // ... 1 / |h_i|
   const float* ndot;     // ... dot_i (reduced dotp)
   int dot_nslot;         // ... > 0: the dZ grid reduces dotp (dot_nslot slots) into ndot itself
+  int dot_spin;          //     polls before dz_dot's fallback (tests: 0 forces the fallback)
   int* dot_cnt;          //     (dz_dot_fold), published through these [2] zeroed counters (self-
                          //     cleaning) to its own epilogues; null for split-K pieces
   const float* ngo;      // ... grad_out (device scalar)
@@ -810,17 +811,18 @@ __device__ __forceinline__ void dz_dot_fold(const SimParams& p, lds_char* lds, i
 // until every block has counted; a poll that runs out (blocks not co-resident: never seen) makes
 // the wave sum the slots itself from then on (state 2), in the same order. sc1 loads (the
 // producer stored sc1: MI355X_MICROARCH.md, visibility, first table row).
-constexpr int kDotSpinBound = 1 << 14;  // x s_sleep 8 (~0.2 us): a few ms
 template <bool FOLD>
 __device__ __forceinline__ float dz_dot(const SimParams& p, int row, int& state) {
   if (!FOLD || p.dot_cnt == nullptr) return p.ndot[row];
   if (state == 0) {
     int n = 0;
-    while (__hip_atomic_load(p.dot_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int)gridDim.x && n < kDotSpinBound) {
+    bool done = false;
+    while (!(done = __hip_atomic_load(p.dot_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) &&
+           n < p.dot_spin) {
       __builtin_amdgcn_s_sleep(8);
       ++n;
     }
-    state = n < kDotSpinBound ? 1 : 2;
+    state = done && p.dot_spin > 0 ? 1 : 2;
   }
   if (state == 2) {  // (serial: dot_slot_sum's additions in the same order, few registers)
     float t = 0.f;

@@ -1153,6 +1153,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("half_c_enabled", &ntxent::half_c_enabled);
   m.def("set_dot_fold", &ntxent::set_dot_fold, py::arg("on"));
   m.def("dot_fold_enabled", &ntxent::dot_fold_enabled);
+  m.def("set_dot_fold_spin", &ntxent::set_dot_fold_spin, py::arg("polls"));
+  m.def("dot_fold_spin", &ntxent::dot_fold_spin);
   m.def("fp8_backward_enabled", &ntxent::fp8_backward_enabled);
   m.def("fwd_splitk_pieces", &ntxent::fwd_splitk_pieces, py::arg("ntiles"), py::arg("nk"), py::arg("cus"),
         py::arg("diag_tail"));

@@ -95,3 +95,18 @@ def test_dot_fold_engine_bitwise(ext):
         assert la == lb
         assert torch.equal(ga, gb)
     assert torch.equal(b[0][1], b[1][1])
+
+
+@pytest.mark.parametrize("rows,dim", [(8192, 2048), (6000, 2048)])
+def test_dot_fold_fallback_bitwise(ext, rows, dim):
+    # every epilogue skips the poll and sums its rows' dot from the slots itself (the path a grid
+    # whose blocks are not all resident would take): the same additions, the same bits
+    h = _views(rows, dim, seed=rows + 3, dtype=torch.bfloat16)
+    spin = ext.dot_fold_spin()
+    try:
+        ext.set_dot_fold_spin(0)
+        (l0, g0), (l1, g1) = _both(ext, lambda: _grad(h, 0.07))
+    finally:
+        ext.set_dot_fold_spin(spin)
+    assert l0.item() == l1.item()
+    assert torch.equal(g0, g1), f"max diff {(g0.float() - g1.float()).abs().max().item()}"
