@@ -781,8 +781,8 @@ __device__ __forceinline__ float dot_slot_sum(const float* dotp, int nslot, int 
 // block of the persistent grid, before its first item, sums dot_i for its share of rows (32-row
 // chunks, dot_reduce_kernel's arithmetic) and stores them sc1; one lane adds 1 to dot_cnt[0]
 // after a block barrier that follows every wave's retirement of those stores. The epilogue's
-// reads (dz_dot) come one whole main loop later. Split-K pieces (no
-// epilogue here: sk_dz_reduce_kernel reads dot after the kernel boundary) fold without the count.
+// reads (dz_dot) come one whole main loop later. Split-K pieces (no epilogue here:
+// sk_dz_reduce_kernel reads dot after the kernel boundary) fold without the count.
 __device__ __forceinline__ void dz_dot_fold(const SimParams& p, lds_char* lds, int tid) {
   typedef __attribute__((address_space(3))) float lds_fl;
   lds_fl* part = (lds_fl*)lds;  // [2 halves][8 slot groups][32 rows]
@@ -1429,7 +1429,7 @@ __global__ __launch_bounds__(kGemmThreads) void sim_gemm_kernel(const SimParams 
   bool dot_counted = false;  // ... this block's fold counted (at its first item)
   if constexpr (MODE == kModeDz && !kF8 && sizeof(T) == 2) {
     // every block (one with no work too) folds its share of the dot reduce before its first item
-    // and counts it once its first prologue wait has retired the stores (dz_dot_signal); inside
+    // and counts it once its first prologue wait has retired the stores (below); inside
     // the item loop the fold put ~30 more SGPR spills around it, and a peeled first prologue
     // (the fold under its DMA) put 4x the lane reads into the K-loop. The fold's LDS (2 KiB) is
     // the epilogue's per-row coefficients.
